@@ -1,0 +1,114 @@
+"""ORACLE (test infrastructure only): Kaldi-compatible log-mel fbank in numpy.
+
+Restates `torchaudio.compliance.kaldi.fbank` (third-party dependency of the
+reference, `requirements.txt` torchaudio>=0.12, unpinned; NOT installed here)
+exactly as the reference calls it:
+
+  * cli/speaker.py:89-104  kaldi.fbank(num_mel_bins=80, frame_length=25,
+    frame_shift=10, sample_frequency=sr, window_type=hamming) then CMN
+    `feat - mean(feat, 0)`; dither / energy at torchaudio defaults (0.0/False).
+  * dataset/processor.py:472-502  same with `wav * (1 << 15)` and dither
+    forced to 0.0 by bin/extract.py:66-67.
+
+Published algorithm (torchaudio compliance/kaldi.py, v0.12-2.x):
+  snip_edges framing (n = 1 + (N - 400) // 160) -> per-frame DC removal ->
+  pre-emphasis 0.97 with replicate pad (x[0] -= 0.97 x[0]) -> symmetric
+  Hamming 0.54 - 0.46 cos(2 pi n / (L-1)) -> zero-pad to 512 -> rFFT ->
+  |X|^2 -> 80 triangular mel filters 20 Hz .. Nyquist (mel = 1127 ln(1+f/700),
+  filter column for the Nyquist bin = 0) -> log(max(e, FLT_EPSILON)).
+
+The reference's own native restatement of the same algorithm is
+runtime/core/frontend/fbank.h:138-198 (+ fft.cc:59-119); it needs glog and is
+therefore not compilable here without a stand-in header, so it is read, not
+built.  **Parity with reference outputs is unpinned** (no fixture holds fbank
+outputs); `fbank()` is cross-checked against `fbank_dft64()` (independent
+float64 direct-DFT formulation) in tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+FLT_EPS = np.float32(np.finfo(np.float32).eps)
+
+
+def mel_scale(f):
+    return 1127.0 * np.log(1.0 + np.asarray(f) / 700.0)
+
+
+def mel_banks(num_bins=80, padded=512, sample_freq=16000.0, low_freq=20.0, high_freq=0.0,
+              dtype=np.float32) -> np.ndarray:
+    """get_mel_banks (torchaudio kaldi.py) — (num_bins, padded//2 + 1) incl. zero Nyquist column."""
+    num_fft_bins = padded // 2
+    nyquist = 0.5 * sample_freq
+    if high_freq <= 0.0:
+        high_freq += nyquist
+    fft_bin_width = sample_freq / padded
+    mel_low = 1127.0 * np.log(1.0 + low_freq / 700.0)
+    mel_high = 1127.0 * np.log(1.0 + high_freq / 700.0)
+    delta = (mel_high - mel_low) / (num_bins + 1)
+    b = np.arange(num_bins, dtype=dtype)[:, None]
+    left = (mel_low + b * dtype(delta)).astype(dtype)
+    center = (mel_low + (b + 1) * dtype(delta)).astype(dtype)
+    right = (mel_low + (b + 2) * dtype(delta)).astype(dtype)
+    freq = (dtype(fft_bin_width) * np.arange(num_fft_bins, dtype=dtype))[None, :]
+    mel = (1127.0 * np.log(dtype(1.0) + freq / dtype(700.0))).astype(dtype)
+    up = (mel - left) / (center - left)
+    down = (right - mel) / (right - center)
+    w = np.maximum(dtype(0), np.minimum(up, down)).astype(dtype)
+    return np.concatenate([w, np.zeros((num_bins, 1), dtype=dtype)], axis=1)
+
+
+def _frames(wave: np.ndarray, frame_len: int, frame_shift: int) -> np.ndarray:
+    n = 1 + (len(wave) - frame_len) // frame_shift
+    idx = np.arange(frame_len)[None, :] + frame_shift * np.arange(n)[:, None]
+    return wave[idx]
+
+
+def _window(frame_len, dtype):
+    n = np.arange(frame_len, dtype=np.float64)
+    return (0.54 - 0.46 * np.cos(2 * np.pi * n / (frame_len - 1))).astype(dtype)
+
+
+def _prep(wave, frame_len, frame_shift, dtype, preemph=0.97):
+    x = _frames(np.asarray(wave, dtype=dtype), frame_len, frame_shift)
+    x = x - x.mean(axis=1, keepdims=True)
+    prev = np.concatenate([x[:, :1], x[:, :-1]], axis=1)
+    x = x - dtype(preemph) * prev
+    return (x * _window(frame_len, dtype)[None, :]).astype(dtype)
+
+
+def fbank(wave, num_mel_bins=80, frame_length_ms=25.0, frame_shift_ms=10.0, sample_freq=16000.0,
+          dtype=np.float64, cmn=False) -> np.ndarray:
+    """(T, num_mel_bins) log-mel, computed in `dtype` with numpy's FFT."""
+    fl = int(sample_freq * frame_length_ms * 0.001)
+    fs = int(sample_freq * frame_shift_ms * 0.001)
+    if len(wave) < fl:
+        return np.zeros((0, num_mel_bins), dtype=np.float32)
+    padded = 1 << int(np.ceil(np.log2(fl)))
+    x = _prep(wave, fl, fs, dtype)
+    spec = np.fft.rfft(x, n=padded, axis=1)
+    power = (spec.real ** 2 + spec.imag ** 2).astype(dtype)
+    banks = mel_banks(num_mel_bins, padded, sample_freq).astype(dtype)
+    mel = power @ banks.T
+    out = np.log(np.maximum(mel, FLT_EPS)).astype(np.float32)
+    if cmn:
+        out = (out - out.mean(axis=0, keepdims=True)).astype(np.float32)
+    return out
+
+
+def fbank_dft64(wave, num_mel_bins=80, sample_freq=16000.0) -> np.ndarray:
+    """Independent float64 formulation (explicit DFT matrix) used to cross-check `fbank`."""
+    fl, fs, padded = 400, 160, 512
+    x = _prep(wave, fl, fs, np.float64)
+    k = np.arange(padded // 2 + 1)[:, None]
+    n = np.arange(fl)[None, :]
+    ang = 2 * np.pi * k * n / padded
+    re = x @ np.cos(ang).T
+    im = -(x @ np.sin(ang).T)
+    power = re * re + im * im
+    mel = power @ mel_banks(num_mel_bins, padded, sample_freq).astype(np.float64).T
+    return np.log(np.maximum(mel, FLT_EPS)).astype(np.float32)
+
+
+def fbank_batch(waves: np.ndarray, cmn=True, dtype=np.float64) -> np.ndarray:
+    return np.stack([fbank(w, dtype=dtype, cmn=cmn) for w in waves])

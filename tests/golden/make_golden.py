@@ -1,0 +1,171 @@
+"""Generate golden fixtures from the REFERENCE implementation (survey container only).
+
+Run once in the container where `/root/reference` exists:
+
+    python tests/golden/make_golden.py
+
+It imports the reference's own model / pooling / scoring code read-only from
+`/root/reference/wespeaker` (package-init bypass documented in SURVEY.md §8(c):
+`wespeaker/__init__.py` imports silero_vad/torchaudio/kaldiio which are absent),
+loads seeded synthetic weights produced by `wespeaker_hubert_amd.synthetic`
+(keyed by parameter name), runs the reference forward on seeded inputs and
+stores ONLY inputs-seeds, input checksums and outputs as `.npz` fixtures.  No
+reference source is copied; nothing under `/root/reference` is needed to *use*
+the fixtures (GPU box included).
+
+Reference call sites exercised:
+  * ECAPA_TDNN_*           wespeaker/models/ecapa_tdnn.py:160-274
+  * ResNet34 / ResNet293   wespeaker/models/resnet.py:110-260
+  * ASTP / TSTP            wespeaker/models/pooling_layers.py:67-148
+  * get_mean_std           wespeaker/bin/score_norm.py:26-36
+  * compute_pmiss_pfa_rbst / compute_eer / compute_c_norm
+                           wespeaker/utils/score_metrics.py:58-105
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from wespeaker_hubert_amd.synthetic import synth_feats, synth_state_dict  # noqa: E402
+
+REF = "/root/reference"
+
+
+def _import_reference():
+    pkg = types.ModuleType("wespeaker")
+    pkg.__path__ = [os.path.join(REF, "wespeaker")]
+    sys.modules["wespeaker"] = pkg
+    # import-only stubs: score_norm imports fire + kaldiio at module level but
+    # get_mean_std never touches them.
+    for stub in ("fire", "kaldiio"):
+        if stub not in sys.modules:
+            sys.modules[stub] = types.ModuleType(stub)
+    from wespeaker.models import ecapa_tdnn, pooling_layers, resnet  # noqa
+    from wespeaker.bin import score_norm  # noqa
+    from wespeaker.utils import score_metrics  # noqa
+    return ecapa_tdnn, resnet, pooling_layers, score_norm, score_metrics
+
+
+def load_synth(model, seed, residual_tame=False):
+    shapes = [(k, tuple(v.shape)) for k, v in model.state_dict().items()]
+    sd = synth_state_dict(seed, shapes, residual_tame=residual_tame)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    model.eval()
+    return model
+
+
+# (fixture name, ctor, ctor kwargs, weight seed, input seed, B, T, residual_tame)
+MODEL_CASES = [
+    ("ecapa_c512_b2_t200", "ECAPA_TDNN_c512", dict(feat_dim=80, embed_dim=192), 11, 101, 2, 200, False),
+    ("ecapa_c512_b1_t301", "ECAPA_TDNN_c512", dict(feat_dim=80, embed_dim=192), 11, 102, 1, 301, False),
+    ("ecapa_glob_c512_b2_t200", "ECAPA_TDNN_GLOB_c512", dict(feat_dim=80, embed_dim=192), 12, 103, 2, 200, False),
+    ("ecapa_glob_c512_embbn_b2_t123", "ECAPA_TDNN_GLOB_c512",
+     dict(feat_dim=80, embed_dim=256, emb_bn=True), 13, 104, 2, 123, False),
+    ("ecapa_c1024_b2_t498", "ECAPA_TDNN_c1024", dict(feat_dim=80, embed_dim=192), 14, 105, 2, 498, False),
+    ("ecapa_glob_c1024_b1_t150", "ECAPA_TDNN_GLOB_c1024", dict(feat_dim=80, embed_dim=192), 15, 106, 1, 150, False),
+    ("ecapa_glob_c512_ssl768_b2_t250", "ECAPA_TDNN_GLOB_c512", dict(feat_dim=768, embed_dim=192), 16, 107, 2, 250, False),
+    ("resnet34_b2_t200", "ResNet34", dict(feat_dim=80, embed_dim=256), 21, 201, 2, 200, True),
+    ("resnet293_b1_t160", "ResNet293", dict(feat_dim=80, embed_dim=256), 22, 202, 1, 160, True),
+]
+
+
+def make_models(out):
+    ecapa_tdnn, resnet, _, _, _ = _import_reference()
+    for name, ctor, kw, wseed, iseed, B, T, tame in MODEL_CASES:
+        mod = ecapa_tdnn if ctor.startswith("ECAPA") else resnet
+        torch.manual_seed(0)
+        model = load_synth(getattr(mod, ctor)(**kw), wseed, residual_tame=tame)
+        x = synth_feats(iseed, B, T, kw["feat_dim"])
+        inter = {}
+        hooks = []
+        if name == "ecapa_c512_b2_t200":
+            for lname in ("layer1", "layer2", "layer3", "layer4", "conv", "pool"):
+                def hook(_m, _i, o, lname=lname):
+                    inter[lname] = o.detach().numpy().copy()
+                hooks.append(getattr(model, lname).register_forward_hook(hook))
+        with torch.no_grad():
+            outs = model(torch.from_numpy(x))
+        emb = outs[-1] if isinstance(outs, tuple) else outs
+        for h in hooks:
+            h.remove()
+        rec = dict(arch=np.array(ctor), weight_seed=np.int64(wseed), input_seed=np.int64(iseed),
+                   B=np.int64(B), T=np.int64(T), feat_dim=np.int64(kw["feat_dim"]),
+                   embed_dim=np.int64(kw["embed_dim"]), emb_bn=np.int64(int(kw.get("emb_bn", False))),
+                   residual_tame=np.int64(int(tame)),
+                   input_sum=np.float64(x.astype(np.float64).sum()), input_head=x.reshape(-1)[:16].copy(),
+                   param_names=np.array([k for k in model.state_dict()]),
+                   param_shapes=np.array([",".join(map(str, v.shape)) for v in model.state_dict().values()]),
+                   embed=emb.numpy().astype(np.float32))
+        if inter:
+            # channels-first (B,C,T) as the reference produces; keep only batch 0
+            for k, v in inter.items():
+                rec["inter_" + k] = v[:1].astype(np.float32)
+        np.savez_compressed(os.path.join(out, name + ".npz"), **rec)
+        print(name, emb.shape, float(emb.abs().max()), float(emb.std()))
+
+
+def make_pooling(out):
+    _, _, pooling_layers, _, _ = _import_reference()
+    rng = np.random.default_rng(301)
+    x = rng.standard_normal((2, 48, 37)).astype(np.float32) * 1.5 + 0.3
+    res = {"x": x}
+    torch.manual_seed(0)
+    for tag, glob in (("astp", False), ("astp_glob", True)):
+        p = pooling_layers.ASTP(in_dim=48, bottleneck_dim=16, global_context_att=glob)
+        shapes = [(k, tuple(v.shape)) for k, v in p.state_dict().items()]
+        sd = synth_state_dict(302 if glob else 303, shapes)
+        p.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        with torch.no_grad():
+            res[tag] = p(torch.from_numpy(x)).numpy()
+        res[tag + "_seed"] = np.int64(302 if glob else 303)
+    x4 = rng.standard_normal((2, 8, 5, 29)).astype(np.float32)
+    res["x4"] = x4
+    with torch.no_grad():
+        res["tstp4"] = pooling_layers.TSTP(in_dim=40)(torch.from_numpy(x4)).numpy()
+        res["tstp3"] = pooling_layers.TSTP(in_dim=48)(torch.from_numpy(x)).numpy()
+    np.savez_compressed(os.path.join(out, "pooling.npz"), **res)
+    print("pooling", {k: v.shape for k, v in res.items() if hasattr(v, "shape")})
+
+
+def make_scoring(out):
+    _, _, _, score_norm, score_metrics = _import_reference()
+    rng = np.random.default_rng(401)
+    D = 64
+    emb = rng.standard_normal((7, D)).astype(np.float32)
+    cohort = rng.standard_normal((500, D)).astype(np.float32)
+    mean_vec = (0.1 * rng.standard_normal(D)).astype(np.float32)
+    mu, sd = score_norm.get_mean_std(emb - mean_vec, cohort - mean_vec, 100)
+    mu_all, sd_all = score_norm.get_mean_std(emb - mean_vec, cohort - mean_vec, 500)
+    # EER / minDCF on synthetic trials
+    n = 3000
+    labels = rng.random(n) < 0.3
+    scores = np.where(labels, rng.normal(0.6, 0.15, n), rng.normal(0.1, 0.15, n))
+    scores = np.round(scores, 5)
+    fnr, fpr = score_metrics.compute_pmiss_pfa_rbst(scores, labels)
+    eer, thres = score_metrics.compute_eer(fnr, fpr, scores)
+    mindcf = score_metrics.compute_c_norm(fnr, fpr, p_target=0.01, c_miss=1, c_fa=1)
+    mindcf5 = score_metrics.compute_c_norm(fnr, fpr, p_target=0.05, c_miss=1, c_fa=1)
+    np.savez_compressed(os.path.join(out, "scoring.npz"), emb=emb, cohort=cohort, mean_vec=mean_vec,
+                        top_n=np.int64(100), mu=mu, sd=sd, mu_all=mu_all, sd_all=sd_all,
+                        scores=scores, labels=labels, eer=np.float64(eer), thres=np.float64(thres),
+                        mindcf=np.float64(mindcf), mindcf5=np.float64(mindcf5))
+    print("scoring eer", eer, "mindcf", mindcf)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(os.cpu_count() or 1)
+    what = sys.argv[1:] or ["models", "pooling", "scoring"]
+    if "pooling" in what:
+        make_pooling(HERE)
+    if "scoring" in what:
+        make_scoring(HERE)
+    if "models" in what:
+        make_models(HERE)

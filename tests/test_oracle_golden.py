@@ -1,0 +1,87 @@
+"""Pin the CPU oracle against golden fixtures made from the reference itself
+(tests/golden/make_golden.py).  CPU only."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import models_ref, scoring_ref
+from wespeaker_hubert_amd import arch as A
+from wespeaker_hubert_amd.synthetic import synth_feats, synth_state_dict
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+MODEL_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLD, "*.npz"))
+                        if os.path.basename(p).startswith(("ecapa", "resnet")))
+
+
+def load_case(path):
+    z = np.load(path, allow_pickle=False)
+    arch = str(z["arch"])
+    spec = A.make_spec(arch, feat_dim=int(z["feat_dim"]), embed_dim=int(z["embed_dim"]),
+                       emb_bn=bool(int(z["emb_bn"])))
+    plist = A.param_list(spec)
+    sd = synth_state_dict(int(z["weight_seed"]), plist, residual_tame=bool(int(z["residual_tame"])))
+    x = synth_feats(int(z["input_seed"]), int(z["B"]), int(z["T"]), int(z["feat_dim"]))
+    return z, spec, plist, sd, x
+
+
+@pytest.mark.parametrize("path", MODEL_FIXTURES, ids=[os.path.basename(p)[:-4] for p in MODEL_FIXTURES])
+def test_param_layout_matches_reference(path):
+    z, spec, plist, _, _ = load_case(path)
+    names = [str(n) for n in z["param_names"]]
+    shapes = [tuple(int(s) for s in str(v).split(",") if s) for v in z["param_shapes"]]
+    assert [n for n, _ in plist] == names
+    assert [tuple(s) for _, s in plist] == shapes
+
+
+@pytest.mark.parametrize("path", MODEL_FIXTURES, ids=[os.path.basename(p)[:-4] for p in MODEL_FIXTURES])
+def test_oracle_matches_reference_forward(path):
+    z, spec, _, sd, x = load_case(path)
+    assert abs(x.astype(np.float64).sum() - float(z["input_sum"])) < 1e-6 * max(1.0, abs(float(z["input_sum"])))
+    np.testing.assert_array_equal(x.reshape(-1)[:16], z["input_head"])
+    sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
+    with torch.no_grad():
+        _, emb = models_ref.forward(spec.arch, torch.from_numpy(x), sdt, emb_bn=spec.emb_bn)
+    ref = z["embed"]
+    assert emb.shape == ref.shape
+    np.testing.assert_allclose(emb.numpy(), ref, atol=2e-5, rtol=0)
+
+
+def test_oracle_ecapa_intermediates():
+    z, spec, _, sd, x = load_case(os.path.join(GOLD, "ecapa_c512_b2_t200.npz"))
+    sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
+    with torch.no_grad():
+        out, _, (o1, o2, o3, o4) = models_ref.ecapa_frame_level(torch.from_numpy(x), sdt)
+    for name, got in (("layer1", o1), ("layer2", o2), ("layer3", o3), ("layer4", o4), ("conv", out)):
+        np.testing.assert_allclose(got[:1].numpy(), z["inter_" + name], atol=2e-5, rtol=1e-5)
+
+
+def test_oracle_pooling():
+    z = np.load(os.path.join(GOLD, "pooling.npz"), allow_pickle=False)
+    x = torch.from_numpy(z["x"])
+    for tag, glob_ in (("astp", False), ("astp_glob", True)):
+        plist = [("linear1.weight", (16, 48 * (3 if glob_ else 1), 1)), ("linear1.bias", (16,)),
+                 ("linear2.weight", (48, 16, 1)), ("linear2.bias", (48,))]
+        sd = {"pool." + k: torch.from_numpy(v) for k, v in synth_state_dict(int(z[tag + "_seed"]), plist).items()}
+        got = models_ref.astp(x, sd, "pool", glob_).numpy()
+        np.testing.assert_allclose(got, z[tag], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(models_ref.tstp(torch.from_numpy(z["x4"])).numpy(), z["tstp4"], atol=1e-6)
+    np.testing.assert_allclose(models_ref.tstp(x).numpy(), z["tstp3"], atol=1e-6)
+
+
+def test_oracle_scoring():
+    z = np.load(os.path.join(GOLD, "scoring.npz"), allow_pickle=False)
+    mv = z["mean_vec"]
+    mu, sd = scoring_ref.get_mean_std(z["emb"] - mv, z["cohort"] - mv, int(z["top_n"]))
+    np.testing.assert_allclose(mu, z["mu"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(sd, z["sd"], rtol=1e-6, atol=1e-7)
+    mu, sd = scoring_ref.get_mean_std(z["emb"] - mv, z["cohort"] - mv, z["cohort"].shape[0])
+    np.testing.assert_allclose(mu, z["mu_all"], rtol=1e-6, atol=1e-7)
+    fnr, fpr = scoring_ref.compute_pmiss_pfa_rbst(z["scores"], z["labels"])
+    eer, thr = scoring_ref.compute_eer(fnr, fpr, z["scores"])
+    assert eer == pytest.approx(float(z["eer"]), abs=1e-12)
+    assert thr == pytest.approx(float(z["thres"]), abs=1e-12)
+    assert scoring_ref.compute_c_norm(fnr, fpr, 0.01) == pytest.approx(float(z["mindcf"]), abs=1e-12)
+    assert scoring_ref.compute_c_norm(fnr, fpr, 0.05) == pytest.approx(float(z["mindcf5"]), abs=1e-12)

@@ -1,0 +1,157 @@
+"""Architecture registry: names, hyper-parameters and state_dict layout.
+
+Mirrors `get_speaker_model(name)(**model_args)` (wespeaker/models/speaker_model.py:30-57)
+for the backbones on the north-star path, and reproduces the exact state_dict
+key/shape list of the reference modules so an `avg_model.pt` trained with the
+reference loads unchanged (`load_checkpoint(strict=False)`,
+wespeaker/utils/checkpoint.py:20-27).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Tuple
+
+ParamList = List[Tuple[str, Tuple[int, ...]]]
+
+ECAPA_ARCHS = {
+    # name: (channels, global_context_att) — ecapa_tdnn.py:237-274
+    "ECAPA_TDNN_c512": (512, False),
+    "ECAPA_TDNN_GLOB_c512": (512, True),
+    "ECAPA_TDNN_c1024": (1024, False),
+    "ECAPA_TDNN_GLOB_c1024": (1024, True),
+}
+RESNET_ARCHS = {
+    # name: (block, num_blocks) — resnet.py:207-260
+    "ResNet18": ("basic", (2, 2, 2, 2)),
+    "ResNet34": ("basic", (3, 4, 6, 3)),
+    "ResNet50": ("bottleneck", (3, 4, 6, 3)),
+    "ResNet101": ("bottleneck", (3, 4, 23, 3)),
+    "ResNet152": ("bottleneck", (3, 8, 36, 3)),
+    "ResNet221": ("bottleneck", (6, 16, 48, 3)),
+    "ResNet293": ("bottleneck", (10, 20, 64, 3)),
+}
+
+
+@dataclass
+class ModelSpec:
+    arch: str
+    feat_dim: int = 80
+    embed_dim: int = 192
+    pooling_func: str = "ASTP"
+    emb_bn: bool = False
+    two_emb_layer: bool = False
+    m_channels: int = 32
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def family(self) -> str:
+        if self.arch.startswith("ECAPA_TDNN"):
+            return "ecapa"
+        if self.arch.startswith("ResNet"):
+            return "resnet"
+        raise KeyError(self.arch)
+
+
+def make_spec(arch: str, **model_args) -> ModelSpec:
+    """`get_speaker_model(arch)(**model_args)` analogue (speaker_model.py:30-57).
+
+    Unknown names raise (the reference prints and exit(1)s, speaker_model.py:55-57).
+    """
+    if arch not in ECAPA_ARCHS and arch not in RESNET_ARCHS:
+        raise KeyError(f"{arch} not found !!! (supported: {sorted(ECAPA_ARCHS) + sorted(RESNET_ARCHS)})")
+    kw = dict(model_args)
+    spec = ModelSpec(arch=arch,
+                     feat_dim=int(kw.pop("feat_dim", 80 if arch.startswith("ECAPA") else 40)),
+                     embed_dim=int(kw.pop("embed_dim", 192 if arch.startswith("ECAPA") else 128)),
+                     pooling_func=kw.pop("pooling_func", "ASTP" if arch.startswith("ECAPA") else "TSTP"),
+                     emb_bn=bool(kw.pop("emb_bn", False)),
+                     two_emb_layer=bool(kw.pop("two_emb_layer", False)))
+    if spec.family == "ecapa" and spec.pooling_func != "ASTP":
+        raise NotImplementedError("ECAPA path implements ASTP pooling (the north-star config)")
+    if spec.family == "resnet" and spec.pooling_func != "TSTP":
+        raise NotImplementedError("ResNet path implements TSTP pooling (the north-star config)")
+    spec.extra = kw
+    return spec
+
+
+def _bn(p: str, c: int) -> ParamList:
+    return [(p + ".weight", (c,)), (p + ".bias", (c,)), (p + ".running_mean", (c,)),
+            (p + ".running_var", (c,)), (p + ".num_batches_tracked", ())]
+
+
+def ecapa_params(spec: ModelSpec) -> ParamList:
+    """state_dict layout of ECAPA_TDNN (ecapa_tdnn.py:160-206)."""
+    C, glob = ECAPA_ARCHS[spec.arch]
+    w = C // 8
+    out: ParamList = [("layer1.conv.weight", (C, spec.feat_dim, 5)), ("layer1.conv.bias", (C,))]
+    out += _bn("layer1.bn", C)
+    for li in (2, 3, 4):
+        p = f"layer{li}.se_res2block"
+        out += [(f"{p}.0.conv.weight", (C, C, 1)), (f"{p}.0.conv.bias", (C,))] + _bn(f"{p}.0.bn", C)
+        for i in range(7):
+            out += [(f"{p}.1.convs.{i}.weight", (w, w, 3)), (f"{p}.1.convs.{i}.bias", (w,))]
+        for i in range(7):
+            out += _bn(f"{p}.1.bns.{i}", w)
+        out += [(f"{p}.2.conv.weight", (C, C, 1)), (f"{p}.2.conv.bias", (C,))] + _bn(f"{p}.2.bn", C)
+        out += [(f"{p}.3.linear1.weight", (128, C)), (f"{p}.3.linear1.bias", (128,)),
+                (f"{p}.3.linear2.weight", (C, 128)), (f"{p}.3.linear2.bias", (C,))]
+    out += [("conv.weight", (1536, 3 * C, 1)), ("conv.bias", (1536,))]
+    out += [("pool.linear1.weight", (128, 1536 * (3 if glob else 1), 1)), ("pool.linear1.bias", (128,)),
+            ("pool.linear2.weight", (1536, 128, 1)), ("pool.linear2.bias", (1536,))]
+    out += _bn("bn", 3072)
+    out += [("linear.weight", (spec.embed_dim, 3072)), ("linear.bias", (spec.embed_dim,))]
+    if spec.emb_bn:
+        out += _bn("bn2", spec.embed_dim)
+    return out
+
+
+def resnet_params(spec: ModelSpec) -> ParamList:
+    """state_dict layout of ResNet (resnet.py:110-169)."""
+    kind, nblocks = RESNET_ARCHS[spec.arch]
+    m = spec.m_channels
+    exp = 1 if kind == "basic" else 4
+    out: ParamList = [("conv1.weight", (m, 1, 3, 3))] + _bn("bn1", m)
+    in_planes = m
+    for li, n in enumerate(nblocks):
+        planes = m * (2 ** li)
+        for bi in range(n):
+            stride = 2 if (li > 0 and bi == 0) else 1
+            p = f"layer{li + 1}.{bi}"
+            if kind == "basic":
+                out += [(p + ".conv1.weight", (planes, in_planes, 3, 3))] + _bn(p + ".bn1", planes)
+                out += [(p + ".conv2.weight", (planes, planes, 3, 3))] + _bn(p + ".bn2", planes)
+            else:
+                out += [(p + ".conv1.weight", (planes, in_planes, 1, 1))] + _bn(p + ".bn1", planes)
+                out += [(p + ".conv2.weight", (planes, planes, 3, 3))] + _bn(p + ".bn2", planes)
+                out += [(p + ".conv3.weight", (planes * 4, planes, 1, 1))] + _bn(p + ".bn3", planes * 4)
+            if stride != 1 or in_planes != exp * planes:
+                out += [(p + ".shortcut.0.weight", (exp * planes, in_planes, 1, 1))]
+                out += _bn(p + ".shortcut.1", exp * planes)
+            in_planes = planes * exp
+    stats_dim = int(spec.feat_dim / 8) * m * 8 * exp
+    out += [("seg_1.weight", (spec.embed_dim, stats_dim * 2)), ("seg_1.bias", (spec.embed_dim,))]
+    if spec.two_emb_layer:
+        out += [("seg_bn_1.running_mean", (spec.embed_dim,)), ("seg_bn_1.running_var", (spec.embed_dim,)),
+                ("seg_bn_1.num_batches_tracked", ()),
+                ("seg_2.weight", (spec.embed_dim, spec.embed_dim)), ("seg_2.bias", (spec.embed_dim,))]
+    return out
+
+
+def param_list(spec: ModelSpec) -> ParamList:
+    return ecapa_params(spec) if spec.family == "ecapa" else resnet_params(spec)
+
+
+def ecapa_gflop_per_utt(spec: ModelSpec, T: int) -> float:
+    """Algorithmic FLOPs (2 x MACs) of one ECAPA forward over T frames."""
+    C, glob = ECAPA_ARCHS[spec.arch]
+    w = C // 8
+    macs = spec.feat_dim * 5 * C * T                       # layer1
+    macs += 3 * (2 * C * C * T + 7 * w * w * 3 * T + 2 * C * 128)  # blocks
+    macs += 3 * C * 1536 * T                                # conv
+    # pool.linear1: GLOB's mean/std context columns are constant over T and
+    # are folded into a per-utterance bias, so both variants run
+    # a 1536-deep contraction per frame.
+    macs += 1536 * 128 * T + (2 * 1536 * 128 if glob else 0)
+    macs += 128 * 1536 * T                                  # pool.linear2
+    macs += 3072 * spec.embed_dim
+    return 2.0 * macs / 1e9

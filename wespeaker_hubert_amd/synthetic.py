@@ -1,0 +1,89 @@
+"""Deterministic synthetic weights and audio for parity tests and the bench.
+
+There are no trained checkpoints offline, so every parity
+fixture and every bench run uses seeded random weights.  The generator is keyed
+by *parameter name* (not by ordering) so that the reference module
+(`wespeaker/models/*.py`, loaded only in the survey container to make golden
+fixtures) and this framework's own loader produce bit-identical tensors from
+the same `(seed, name, shape)`.
+
+Distributions follow SURVEY.md §8(d): conv/linear weights ~ N(0, 1/fan_in),
+BN running_mean ~ N(0, 0.1), running_var ~ U(0.5, 1.5).
+"""
+from __future__ import annotations
+
+import zlib
+from typing import Dict, Iterable, Tuple
+
+import numpy as np
+
+__all__ = ["param_rng", "synth_param", "synth_state_dict", "synth_audio", "synth_feats"]
+
+
+def param_rng(seed: int, name: str) -> np.random.Generator:
+    return np.random.default_rng([int(seed) & 0x7FFFFFFF, zlib.crc32(name.encode("utf-8"))])
+
+
+def synth_param(seed: int, name: str, shape: Tuple[int, ...]) -> np.ndarray:
+    """One parameter / buffer of a state_dict, float32 (int64 for counters)."""
+    shape = tuple(int(s) for s in shape)
+    rng = param_rng(seed, name)
+    leaf = name.rsplit(".", 1)[-1]
+    if leaf == "num_batches_tracked":
+        return np.zeros(shape, dtype=np.int64)
+    if leaf == "running_mean":
+        return (0.1 * rng.standard_normal(shape)).astype(np.float32)
+    if leaf == "running_var":
+        return rng.uniform(0.5, 1.5, shape).astype(np.float32)
+    is_norm = (".bn" in name or name.startswith("bn") or ".norm" in name
+               or "layer_norm" in name or "bns." in name or "seg_bn" in name)
+    if leaf == "weight" and len(shape) == 1:
+        # BatchNorm / LayerNorm / GroupNorm affine scale
+        return rng.uniform(0.8, 1.2, shape).astype(np.float32)
+    if leaf == "bias" and (len(shape) == 1 and is_norm):
+        return (0.1 * rng.standard_normal(shape)).astype(np.float32)
+    if leaf == "bias":
+        return (0.05 * rng.standard_normal(shape)).astype(np.float32)
+    if len(shape) >= 2:
+        fan_in = int(np.prod(shape[1:]))
+        gain = 1.0
+        # Keep deep residual stacks (ResNet293: 90 blocks) numerically tame:
+        # the last BN of every bottleneck / basic block is shrunk, the
+        # usual "small residual branch" initialisation.
+        return (gain * rng.standard_normal(shape) / np.sqrt(fan_in)).astype(np.float32)
+    return (0.05 * rng.standard_normal(shape)).astype(np.float32)
+
+
+def _residual_tame(name: str, arr: np.ndarray) -> np.ndarray:
+    # ResNet blocks: shrink the affine scale of the BN that closes a residual
+    # branch (bn2 of BasicBlock, bn3 of Bottleneck) so 90 stacked residual
+    # adds stay O(1).
+    if name.endswith("bn3.weight") or (".bn2.weight" in name and "layer" in name):
+        return (arr * 0.25).astype(arr.dtype)
+    return arr
+
+
+def synth_state_dict(seed: int, shapes: Iterable[Tuple[str, Tuple[int, ...]]],
+                     residual_tame: bool = False) -> Dict[str, np.ndarray]:
+    out = {}
+    for name, shape in shapes:
+        arr = synth_param(seed, name, shape)
+        if residual_tame:
+            arr = _residual_tame(name, arr)
+        out[name] = arr
+    return out
+
+
+def synth_audio(seed: int, batch: int, num_samples: int, int16_scale: bool = True) -> np.ndarray:
+    """clip(N(0, 0.1), -1, 1) audio; x32768 and rounded to
+    integers for the fbank paths (mimics PCM16 read with normalize=False)."""
+    rng = np.random.default_rng(int(seed))
+    wav = np.clip(0.1 * rng.standard_normal((batch, num_samples)), -1.0, 1.0)
+    if int16_scale:
+        wav = np.round(wav * 32768.0).clip(-32768, 32767)
+    return wav.astype(np.float32)
+
+
+def synth_feats(seed: int, batch: int, frames: int, dim: int) -> np.ndarray:
+    rng = np.random.default_rng(int(seed))
+    return rng.standard_normal((batch, frames, dim)).astype(np.float32)
