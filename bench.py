@@ -1,0 +1,185 @@
+"""Headline benchmark: embeddings/sec on synthetic 5 s 16 kHz utterances.
+
+Workload (BASELINE.json configs[1], C2): ECAPA_TDNN_c1024, Kaldi fbank80 front
+end, batch 256 x 80 000-sample utterances per GPU, resident in HBM before the
+timed region.  One step = fbank + CMN + ECAPA forward + embedding for the whole
+batch, all in libwsp_hip.so.  Multi-GPU: one rank per GPU (torchrun), each
+rank extracts its own shard (weak scaling, no data-path collective).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from wespeaker_hubert_amd.arch import ecapa_gflop_per_utt, make_spec  # noqa: E402
+from wespeaker_hubert_amd.frontend import compute_fbank  # noqa: E402
+from wespeaker_hubert_amd.speaker_model import HipSpeakerModel  # noqa: E402
+from wespeaker_hubert_amd.synthetic import synth_audio, synth_state_dict  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBPS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--arch", default="ECAPA_TDNN_c1024")
+    ap.add_argument("--seconds", type=float, default=5.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing pass")
+    return ap.parse_args()
+
+
+def cpu_baseline(arch: str, sd, num_samples: int, budget_s: float):
+    """Oracle ('port') pipeline timed on the host cores: numpy float64 fbank +
+    CMN, then the fp32 PyTorch-CPU restatement of the reference ECAPA forward.
+    Bounded sample: batches of 8 utterances until >= budget_s of work."""
+    from oracle import fbank_ref, models_ref
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
+
+    def run(n, seed):
+        wav = synth_audio(seed, n, num_samples)
+        feats = np.stack([fbank_ref.fbank(w, cmn=True) for w in wav])
+        with torch.no_grad():
+            models_ref.forward(arch, torch.from_numpy(feats), sdt)
+
+    run(2, 1000)  # warm-up
+    done, t0 = 0, time.perf_counter()
+    while True:
+        run(8, 1001 + done)
+        done += 8
+        el = time.perf_counter() - t0
+        if el >= budget_s or done >= 256:
+            break
+    return {"value": done / el, "unit": "emb/s", "cores": threads, "kind": "port",
+            "sample": f"{done} synthetic {num_samples / 16000:.0f}s utts, batches of 8, "
+                      f"numpy-f64 fbank + torch-CPU fp32 {arch} (oracle restatement), {el:.1f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    B = args.batch
+    N = int(round(args.seconds * 16000))
+    spec = make_spec(args.arch, feat_dim=80, embed_dim=192)
+    model = HipSpeakerModel(args.arch, feat_dim=80, embed_dim=192)
+    sd = synth_state_dict(1234, model.state_dict_layout())
+    model.load_state_dict(sd)
+    model.to(dev)
+
+    # inputs resident in HBM before the timed region (per-rank shard)
+    wav = torch.from_numpy(synth_audio(7 + rank, B, N)).to(dev)
+    T = 1 + (N - 400) // 160
+    feats = torch.empty(B, T, 80, device=dev)
+    emb = torch.empty(B, 192, device=dev)
+
+    def step():
+        compute_fbank(wav, scale=1.0, cmn=True, out=feats)
+        model.embed(feats, out=emb)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    # Per-kernel-class HIP events are recorded on the launch stream around
+    # every launch inside the timed region (wsp_model_profile); they feed the
+    # roofline figure below.
+    if not args.no_profile:
+        model.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    el = time.perf_counter() - t0
+    if not args.no_profile:
+        model.profile(False)
+    if dist is not None:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    value = world * B * args.steps / el
+
+    kernels, roof = {}, None
+    if not args.no_profile:
+        for tag in ("layer1", "conv1x1_CxC", "res2_k3", "se", "conv_cat", "glob_ctx", "pool_linear1",
+                    "pool_linear2", "astp", "head"):
+            n, ms, fl = model.profile_query(tag)
+            if n:
+                avg = ms / n
+                kernels[tag] = {"launches_per_step": n // args.steps, "avg_ms": round(avg, 4),
+                                "ms_per_step": round(ms / args.steps, 4),
+                                "tflops": round(fl / (avg * 1e-3) / 1e12, 2) if fl else None}
+        k = kernels.get("conv1x1_CxC")
+        if k:
+            C = 1024 if "c1024" in args.arch else 512
+            flops = 2.0 * B * T * C * C          # algorithmic: 2*M*N*K, M = B*T frames
+            ach = flops / (k["avg_ms"] * 1e-3) / 1e12
+            roof = {"kernel": "conv_gemm_f32<2,2,2,2,kACat> (SE-Res2Block 1x1 conv CxC)",
+                    "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                    "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"]}
+
+    gf = ecapa_gflop_per_utt(spec, T)
+    res = {
+        "metric": "embeddings/sec on 5s 16kHz utts",
+        "value": round(value, 2),
+        "unit": "emb/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (clip(N(0,0.1)) x32768 PCM16-valued audio, seeded random-init weights)",
+        "config": {"workload": f"{args.arch} fbank80 extract, {args.seconds:g}s 16kHz utts",
+                   "arch": args.arch, "batch_per_gpu": B, "global_batch": B * world,
+                   "samples_per_utt": N, "frames": T, "parallelism": f"dp{world}"},
+        "model_tflops": round(value * gf / 1e3, 2),
+        "gflop_per_utt": round(gf, 3),
+        "roofline": roof,
+        "kernels": kernels,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(args.arch, sd, N, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

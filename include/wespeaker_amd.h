@@ -1,0 +1,132 @@
+/*
+ * wespeaker_amd.h — C-ABI of the MI355X-native speaker-embedding extraction
+ * path (libwsp_hip.so).  Plain pointers and sizes only; no torch types.
+ *
+ * Device pointers are HIP device pointers (e.g. torch.Tensor.data_ptr() of a
+ * cuda tensor); `stream` is a hipStream_t passed as void* (NULL = default
+ * stream).  Every entry point returns 0 on success or a negative WSP_E* code;
+ * the message of the last failure on the calling thread is wsp_last_error().
+ * The library never frees caller memory and never synchronises the stream
+ * except where a function says so.  A model handle is bound to the device
+ * that was current when it was created; it is thread-compatible, not
+ * thread-safe.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference repository JunyiPeng00/wespeaker_hubert):
+ *   wsp_fbank            torchaudio.compliance.kaldi.fbank as called at
+ *                        wespeaker/cli/speaker.py:89-104 and
+ *                        wespeaker/dataset/processor.py:472-502 (+ CMN of
+ *                        speaker.py:102-103 / dataset_utils.py:19-26);
+ *                        native restatement runtime/core/frontend/fbank.h:138-198
+ *   wsp_model_*          get_speaker_model(name)(**model_args) + load_checkpoint
+ *                        (wespeaker/models/speaker_model.py:30-57,
+ *                        wespeaker/utils/checkpoint.py:20-27) and the
+ *                        `model(feats)[-1]` forward (cli/speaker.py:164-167,
+ *                        bin/extract.py:114-116); C++ plugin analogue
+ *                        SpeakerModel::ExtractEmbedding
+ *                        (runtime/core/speaker/speaker_model.h:25-32)
+ *   wsp_l2_normalize,
+ *   wsp_cosine_pairs     bin/score.py:38-72 trials_cosine_score;
+ *                        Speaker.cosine_similarity cli/speaker.py:189-192
+ *   wsp_asnorm_stats     bin/score_norm.py:26-36 get_mean_std
+ *   wsp_row_mean_accum   bin/score.py:25-35 calculate_mean_from_kaldi_vec,
+ *                        tools/vector_mean.py:24-53 compute_vector_mean
+ */
+#ifndef WESPEAKER_AMD_H_
+#define WESPEAKER_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WSP_OK 0
+#define WSP_E_INVALID (-1)   /* bad argument / shape */
+#define WSP_E_HIP (-2)       /* HIP runtime error */
+#define WSP_E_STATE (-3)     /* call order (e.g. forward before finalize) */
+#define WSP_E_UNSUPPORTED (-4)
+
+#define WSP_DTYPE_F32 0
+#define WSP_DTYPE_S16 1
+
+#define WSP_WINDOW_HAMMING 0
+#define WSP_WINDOW_POVEY 1
+
+typedef struct wsp_model wsp_model;
+
+int wsp_abi_version(void);
+const char* wsp_last_error(void);
+
+/* ------------------------------------------------------------- fbank --- */
+/* Number of snip-edges frames: 1 + (num_samples - frame_len) / frame_shift,
+ * 0 when num_samples < frame_len. */
+int wsp_fbank_num_frames(int num_samples, int frame_len, int frame_shift);
+
+/* Batched Kaldi log-mel fbank (80 bins, 25 ms / 10 ms @16 kHz, 512-pt FFT,
+ * dither 0, DC removal, pre-emphasis 0.97, hamming window).
+ *   wav    [B][ld] samples (f32 or s16), first num_samples of each row used
+ *   scale  multiplies samples first (32768 for [-1,1] input on the
+ *          dataset path, processor.py:492; 1 for int16-valued input)
+ *   feats  [B][T][num_bins] f32, T = wsp_fbank_num_frames(num_samples,...)
+ *   cmn    1: subtract the per-utterance mean over frames (speaker.py:102-103)
+ * Only num_bins = 80, sample_rate = 16000, frame 400 / shift 160 and the
+ * hamming window are implemented (the north-star configuration). */
+int wsp_fbank(const void* wav, int wav_dtype, int B, int num_samples, int ld, float scale,
+              float* feats, int num_bins, int sample_rate, int window_type, int cmn,
+              void* stream);
+
+/* ------------------------------------------------------------- model --- */
+/* arch: "ECAPA_TDNN_c512", "ECAPA_TDNN_GLOB_c512", "ECAPA_TDNN_c1024",
+ * "ECAPA_TDNN_GLOB_c1024", "ResNet18/34/50/101/152/221/293" */
+int wsp_model_create(const char* arch, int feat_dim, int embed_dim, int emb_bn,
+                     int two_emb_layer, wsp_model** out);
+int wsp_model_destroy(wsp_model* m);
+/* Parameters follow the reference state_dict order (wsp_model_param_info). */
+int wsp_model_num_params(const wsp_model* m);
+int wsp_model_param_info(const wsp_model* m, int index, const char** name, int* ndim,
+                         int64_t shape[4]);
+/* Copy one parameter from HOST memory (float32, numel elements). */
+int wsp_model_set_param(wsp_model* m, int index, const float* host_data, int64_t numel);
+/* Fold BatchNorms, pack weights for the kernels, upload.  Synchronous. */
+int wsp_model_finalize(wsp_model* m);
+int wsp_model_embed_dim(const wsp_model* m);
+int wsp_model_feat_dim(const wsp_model* m);
+/* Bytes of device workspace a forward over B utterances of T frames needs. */
+int wsp_model_workspace_bytes(const wsp_model* m, int B, int T, size_t* bytes);
+/* feats [B][T][feat_dim] f32 (channels-last, exactly the reference's (B,T,F)
+ * input) -> embed [B][embed_dim] f32.  Asynchronous on `stream`. */
+int wsp_model_forward(wsp_model* m, const float* feats, int B, int T, float* embed,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* Per-kernel-class timing with HIP events recorded on the launch stream
+ * around every launch (used by bench.py for the roofline figure). */
+int wsp_model_profile(wsp_model* m, int enable);
+/* Synchronises the events; returns launches, summed ms and algorithmic
+ * FLOPs per launch of the named kernel class, then clears it. */
+int wsp_model_profile_query(wsp_model* m, const char* kernel_class, int* launches,
+                            double* total_ms, double* flops_per_launch);
+
+/* ------------------------------------------------------------ scoring --- */
+/* y[r] = x[r] - sub (sub may be NULL), then L2-normalised; [R][D] f32. */
+int wsp_l2_normalize(const float* x, const float* sub, float* y, int R, int D, void* stream);
+/* score[p] = cos(E[idx_a[p]], E[idx_b[p]]) for P pairs (E rows need not be
+ * normalised; accumulation in f64 like sklearn). */
+int wsp_cosine_pairs(const float* E, int D, const int32_t* idx_a, const int32_t* idx_b,
+                     int P, double* score, void* stream);
+/* AS-Norm statistics (get_mean_std): E [Ne][D], C [Nc][D] (both already
+ * L2-normalised), top_n <= Nc.  mu/sd [Ne] f64 (sd: population std). */
+int wsp_asnorm_stats(const float* E, int Ne, const float* C, int Nc, int D, int top_n,
+                     double* mu, double* sd, void* workspace, size_t workspace_bytes,
+                     void* stream);
+int wsp_asnorm_workspace_bytes(int Ne, int Nc, int D, size_t* bytes);
+/* acc[group[r]][:] += x[r][:] (f64), cnt[group[r]] += 1 — per-speaker /
+ * global embedding sums for mean vectors and cohorts. */
+int wsp_row_mean_accum(const float* x, const int32_t* group, int R, int D, double* acc,
+                       double* cnt, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WESPEAKER_AMD_H_ */

@@ -1,0 +1,57 @@
+"""CPU-only checks of the C-ABI library: it loads without a GPU and exports
+every symbol include/wespeaker_amd.h declares (no compute calls)."""
+import ctypes
+import os
+import re
+
+from wespeaker_hubert_amd import _lib
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(__file__)), "include", "wespeaker_amd.h")
+
+
+def header_symbols():
+    txt = open(HDR).read()
+    return sorted(set(re.findall(r"\b(wsp_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
+
+
+def test_pure_host_entry_points():
+    lib = _lib.load()
+    assert lib.wsp_abi_version() == 1
+    assert lib.wsp_fbank_num_frames(80000, 400, 160) == 498
+    assert lib.wsp_fbank_num_frames(399, 400, 160) == 0
+    assert lib.wsp_fbank_num_frames(400, 400, 160) == 1
+    # model creation / parameter layout is host-only until finalize()
+    h = ctypes.c_void_p()
+    st = lib.wsp_model_create(b"ECAPA_TDNN_c512", 80, 192, 0, 0, ctypes.byref(h))
+    if st != 0:  # hipGetDevice without a GPU may fail: the error must be reported, not crash
+        assert lib.wsp_last_error()
+        return
+    n = lib.wsp_model_num_params(h)
+    from wespeaker_hubert_amd.arch import make_spec, param_list
+    plist = param_list(make_spec("ECAPA_TDNN_c512", feat_dim=80, embed_dim=192))
+    assert n == len(plist)
+    name = ctypes.c_char_p()
+    nd = ctypes.c_int()
+    shp = (ctypes.c_int64 * 4)()
+    for i, (pn, ps) in enumerate(plist):
+        assert lib.wsp_model_param_info(h, i, ctypes.byref(name), ctypes.byref(nd), shp) == 0
+        assert name.value.decode() == pn
+        assert tuple(shp[d] for d in range(nd.value)) == tuple(ps)
+    assert lib.wsp_model_forward(h, None, 1, 10, None, None, 0, None) != 0
+    assert b"null" in lib.wsp_last_error()
+    lib.wsp_model_destroy(h)
+
+
+def test_unknown_arch_is_an_error():
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.wsp_model_create(b"NOPE", 80, 192, 0, 0, ctypes.byref(h)) != 0

@@ -1,0 +1,82 @@
+"""ctypes binding of libwsp_hip.so (include/wespeaker_amd.h).
+
+The HIP library is the product path.  There is no CPU fallback: if the shared
+library is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libwsp_hip.so")
+
+WSP_DTYPE_F32 = 0
+WSP_DTYPE_S16 = 1
+WSP_WINDOW_HAMMING = 0
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "wsp_abi_version": (c_int, []),
+    "wsp_last_error": (c_char_p, []),
+    "wsp_fbank_num_frames": (c_int, [c_int, c_int, c_int]),
+    "wsp_fbank": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int,
+                          c_int, c_int, c_void_p]),
+    "wsp_model_create": (c_int, [c_char_p, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "wsp_model_destroy": (c_int, [c_void_p]),
+    "wsp_model_num_params": (c_int, [c_void_p]),
+    "wsp_model_param_info": (c_int, [c_void_p, c_int, POINTER(c_char_p), POINTER(c_int),
+                                     POINTER(c_int64)]),
+    "wsp_model_set_param": (c_int, [c_void_p, c_int, c_void_p, c_int64]),
+    "wsp_model_finalize": (c_int, [c_void_p]),
+    "wsp_model_embed_dim": (c_int, [c_void_p]),
+    "wsp_model_feat_dim": (c_int, [c_void_p]),
+    "wsp_model_workspace_bytes": (c_int, [c_void_p, c_int, c_int, POINTER(c_size_t)]),
+    "wsp_model_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_size_t,
+                                  c_void_p]),
+    "wsp_model_profile": (c_int, [c_void_p, c_int]),
+    "wsp_model_profile_query": (c_int, [c_void_p, c_char_p, POINTER(c_int), POINTER(c_double),
+                                        POINTER(c_double)]),
+    "wsp_l2_normalize": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "wsp_cosine_pairs": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "wsp_asnorm_stats": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p, c_size_t, c_void_p]),
+    "wsp_asnorm_workspace_bytes": (c_int, [c_int, c_int, c_int, POINTER(c_size_t)]),
+    "wsp_row_mean_accum": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+class WspError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) the HIP library; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise WspError(f"HIP library not built: {LIB_PATH} is missing "
+                       "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = load().wsp_last_error().decode("utf-8", "replace")
+        raise WspError(f"{what} failed (status {status}): {msg}")
+
+
+def call(name: str, *args) -> int:
+    st = getattr(load(), name)(*args)
+    check(st, name)
+    return st

@@ -1,0 +1,210 @@
+// extern "C" boundary (include/wespeaker_amd.h): argument checks, exception
+// -> status translation, thread-local last error.
+#include "../../include/wespeaker_amd.h"
+
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "model.h"
+
+namespace wsp {
+static thread_local std::string g_err;
+void set_error(const std::string& m) { g_err = m; }
+const std::string& get_error() { return g_err; }
+
+// fbank tables, one device copy per device
+static const float* fbank_tables_dev() {
+  static std::mutex mu;
+  static std::vector<float*> per_dev;
+  int dev = 0;
+  WSP_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1, nullptr);
+  if (!per_dev[dev]) {
+    std::vector<float> h(kFbankTableFloats);
+    fbank_tables(h.data());
+    float* d = nullptr;
+    WSP_HIP(hipMalloc(&d, h.size() * sizeof(float)));
+    WSP_HIP(hipMemcpy(d, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    per_dev[dev] = d;
+  }
+  return per_dev[dev];
+}
+}  // namespace wsp
+
+struct wsp_model {
+  wsp::Model m;
+};
+
+#define WSP_GUARD(...)                                                           \
+  try {                                                                          \
+    __VA_ARGS__;                                                                      \
+    return WSP_OK;                                                               \
+  } catch (const wsp::InvalidArg& e) {                                           \
+    wsp::set_error(e.msg);                                                       \
+    return WSP_E_INVALID;                                                        \
+  } catch (const wsp::HipError& e) {                                             \
+    wsp::set_error(std::string("HIP error ") + hipGetErrorString(e.err) + " at " + e.where); \
+    return WSP_E_HIP;                                                            \
+  } catch (const std::exception& e) {                                            \
+    wsp::set_error(e.what());                                                    \
+    return WSP_E_STATE;                                                          \
+  }
+
+static hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+extern "C" {
+
+int wsp_abi_version(void) { return 1; }
+const char* wsp_last_error(void) { return wsp::get_error().c_str(); }
+
+int wsp_fbank_num_frames(int num_samples, int frame_len, int frame_shift) {
+  if (frame_len <= 0 || frame_shift <= 0 || num_samples < frame_len) return 0;
+  return 1 + (num_samples - frame_len) / frame_shift;
+}
+
+int wsp_fbank(const void* wav, int wav_dtype, int B, int num_samples, int ld, float scale,
+              float* feats, int num_bins, int sample_rate, int window_type, int cmn,
+              void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(num_bins == 80, "fbank: only num_mel_bins=80 is implemented");
+    WSP_CHECK(sample_rate == 16000, "fbank: only 16 kHz is implemented");
+    WSP_CHECK(window_type == WSP_WINDOW_HAMMING, "fbank: only the hamming window is implemented");
+    WSP_CHECK(wav_dtype == WSP_DTYPE_F32 || wav_dtype == WSP_DTYPE_S16, "fbank: bad dtype");
+    WSP_CHECK(B >= 0 && num_samples >= 0 && ld >= num_samples, "fbank: bad shape");
+    const int T = wsp_fbank_num_frames(num_samples, 400, 160);
+    if (B > 0 && T > 0) {
+      WSP_CHECK(wav && feats, "fbank: null pointer");
+      wsp::launch_fbank(wav, wav_dtype, B, num_samples, ld, scale, feats, T, cmn,
+                        wsp::fbank_tables_dev(), S(stream));
+    }
+  });
+}
+
+int wsp_model_create(const char* arch, int feat_dim, int embed_dim, int emb_bn, int two_emb_layer,
+                     wsp_model** out) {
+  WSP_GUARD({
+    WSP_CHECK(arch && out, "null argument");
+    auto* h = new wsp_model();
+    try {
+      h->m.create(arch, feat_dim, embed_dim, emb_bn != 0, two_emb_layer != 0);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int wsp_model_destroy(wsp_model* m) {
+  delete m;
+  return WSP_OK;
+}
+
+int wsp_model_num_params(const wsp_model* m) { return m ? m->m.num_params() : WSP_E_INVALID; }
+
+int wsp_model_param_info(const wsp_model* m, int index, const char** name, int* ndim,
+                         int64_t shape[4]) {
+  WSP_GUARD({
+    WSP_CHECK(m && name && ndim && shape, "null argument");
+    m->m.param_info(index, name, ndim, shape);
+  });
+}
+
+int wsp_model_set_param(wsp_model* m, int index, const float* host_data, int64_t numel) {
+  WSP_GUARD({
+    WSP_CHECK(m && (host_data || numel == 0), "null argument");
+    m->m.set_param(index, host_data, numel);
+  });
+}
+
+int wsp_model_finalize(wsp_model* m) {
+  WSP_GUARD({
+    WSP_CHECK(m, "null model");
+    m->m.finalize();
+  });
+}
+
+int wsp_model_embed_dim(const wsp_model* m) { return m ? m->m.embed_dim() : WSP_E_INVALID; }
+int wsp_model_feat_dim(const wsp_model* m) { return m ? m->m.feat_dim() : WSP_E_INVALID; }
+
+int wsp_model_workspace_bytes(const wsp_model* m, int B, int T, size_t* bytes) {
+  WSP_GUARD({
+    WSP_CHECK(m && bytes && B >= 0 && T >= 0, "bad argument");
+    *bytes = m->m.workspace_bytes(B, T);
+  });
+}
+
+int wsp_model_forward(wsp_model* m, const float* feats, int B, int T, float* embed, void* workspace,
+                      size_t workspace_bytes, void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(m && feats && embed && workspace, "null argument");
+    m->m.forward(feats, B, T, embed, workspace, workspace_bytes, S(stream));
+  });
+}
+
+int wsp_model_profile(wsp_model* m, int enable) {
+  WSP_GUARD({
+    WSP_CHECK(m, "null model");
+    m->m.profile(enable != 0);
+  });
+}
+
+int wsp_model_profile_query(wsp_model* m, const char* kernel_class, int* launches,
+                            double* total_ms, double* flops_per_launch) {
+  WSP_GUARD({
+    WSP_CHECK(m && kernel_class && launches && total_ms && flops_per_launch, "null argument");
+    m->m.profile_query(kernel_class, launches, total_ms, flops_per_launch);
+  });
+}
+
+int wsp_l2_normalize(const float* x, const float* sub, float* y, int R, int D, void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(R >= 0 && D > 0 && (R == 0 || (x && y)), "bad argument");
+    wsp::launch_l2_normalize(x, sub, y, R, D, S(stream));
+  });
+}
+
+int wsp_cosine_pairs(const float* E, int D, const int32_t* idx_a, const int32_t* idx_b, int P,
+                     double* score, void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(P >= 0 && D > 0 && (P == 0 || (E && idx_a && idx_b && score)), "bad argument");
+    wsp::launch_cosine_pairs(E, D, idx_a, idx_b, P, score, S(stream));
+  });
+}
+
+int wsp_asnorm_workspace_bytes(int Ne, int Nc, int D, size_t* bytes) {
+  WSP_GUARD({
+    WSP_CHECK(bytes && Ne >= 0 && Nc > 0 && D > 0, "bad argument");
+    int a, b;
+    wsp::asnorm_layout(Ne, Nc, D, &a, &b, bytes);
+  });
+}
+
+int wsp_asnorm_stats(const float* E, int Ne, const float* C, int Nc, int D, int top_n, double* mu,
+                     double* sd, void* workspace, size_t workspace_bytes, void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(Ne >= 0 && Nc > 0 && D > 0, "bad argument");
+    if (Ne == 0) return WSP_OK;
+    int Ncp, Dp;
+    size_t need;
+    wsp::asnorm_layout(Ne, Nc, D, &Ncp, &Dp, &need);
+    WSP_CHECK(workspace && workspace_bytes >= need, "asnorm: workspace too small");
+    wsp::launch_asnorm_stats(E, Ne, C, Nc, D, top_n, mu, sd, static_cast<float*>(workspace),
+                             S(stream));
+  });
+}
+
+int wsp_row_mean_accum(const float* x, const int32_t* group, int R, int D, double* acc,
+                       double* cnt, void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(R >= 0 && D > 0 && (R == 0 || (x && group && acc && cnt)), "bad argument");
+    wsp::launch_row_mean_accum(x, group, R, D, acc, cnt, S(stream));
+  });
+}
+
+}  // extern "C"

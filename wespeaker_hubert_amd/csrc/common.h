@@ -1,0 +1,62 @@
+// Shared helpers for the gfx950 kernels and the C-ABI runtime.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+namespace wsp {
+
+void set_error(const std::string& msg);
+const std::string& get_error();
+
+struct HipError {
+  hipError_t err;
+  std::string where;
+};
+
+#define WSP_HIP(expr)                                                        \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess) throw ::wsp::HipError{_e, std::string(#expr)};     \
+  } while (0)
+
+struct InvalidArg {
+  std::string msg;
+};
+
+#define WSP_CHECK(cond, msg)                                                 \
+  do {                                                                       \
+    if (!(cond)) throw ::wsp::InvalidArg{std::string(msg)};                  \
+  } while (0)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5 / T1): blocks
+// b and b+8 share an XCD under round-robin dispatch, so give each XCD a
+// contiguous range of logical tile ids.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int start = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return start + (bid >> 3);
+}
+
+inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace wsp

@@ -1,0 +1,217 @@
+// Implicit-GEMM conv1d on gfx950 f32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Replaces the nn.Conv1d calls of the reference ECAPA-TDNN
+// (wespeaker/models/ecapa_tdnn.py:85-106 Conv1dReluBn, :29-78 Res2Conv1dReluBn,
+// :203 self.conv, pooling_layers.py:105-117 ASTP linear1/linear2), fused with
+// the bias / ReLU / eval-BatchNorm / tanh epilogues that follow them.
+//
+// Precision: exact fp32 products and fp32 accumulation (the f32-input MFMA is
+// a k-ordered fmaf chain, cdna_hip_programming.md §3), so the result differs
+// from PyTorch's CPU conv only by summation order.
+//
+// Tiling (256 threads = 4 waves, one 32x32 MFMA tile grid per wave):
+//   block BM x BN x BK=32, waves WM x WN, each wave TM x TN tiles of 32x32.
+//   LDS: A tile [BM][36] and B tile [BN][36] (k contiguous, +4 pad), double
+//   buffered; a lane reads 4 consecutive k of one row with ds_read_b128 and
+//   feeds 4 MFMA steps: MFMA step s of half h (lane>>5) contracts k = 16h + s,
+//   the same permutation on both operands (conflict-free: row stride 9 slots).
+//   Global->LDS staging is register-staged float4 (128-B row segments),
+//   issued before the MFMA block and written after it (cdna guide T14).
+#include "kernels.h"
+
+namespace wsp {
+
+namespace {
+
+constexpr int BK = 32;
+constexpr int LDK = BK + 4;
+
+template <int WM, int WN, int TM, int TN, int AMODE>
+__global__ __launch_bounds__(256, 2) void conv_gemm_f32(const ConvGemmArgs p) {
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int AR = BM / 32;  // float4 A loads per thread per k-tile
+  constexpr int BR = BN / 32;  // float4 B loads per thread per k-tile
+  static_assert(WM * WN == 4, "4 waves");
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* As = smem;                  // [2][BM][LDK]
+  float* Bs = smem + 2 * BM * LDK;   // [2][BN][LDK]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int ntiles = p.N / BN;
+  const int mtiles = (p.M + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, ntiles * mtiles);
+  const int mt = wg / ntiles;
+  const int nt = wg - mt * ntiles;
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
+
+  // ---- staging geometry: thread loads rows (tid>>3) + 32 i, k-chunk (tid&7)
+  const int srow = tid >> 3;
+  const int c4 = (tid & 7) * 4;
+  int a_m[AR], a_t[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + srow + 32 * i;
+    a_m[i] = m;
+    a_t[i] = (m < p.M) ? (m % p.T) : -0x40000000;  // invalid rows never pass the t-range test
+  }
+  const float* wrow[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) wrow[i] = p.w + (size_t)(n0 + srow + 32 * i) * p.Kp + c4;
+
+  f32x4 ra[AR], rb[BR];
+
+  auto load_tile = [&](int k0) {
+    const int k = k0 + c4;
+    int j = 0, c = 0;
+    bool kin = k < p.K;
+    if (kin) {
+      j = k / p.cin;
+      c = k - j * p.cin;
+    }
+    const int off = j * p.dil - p.pad;
+    int seg = 0, cl = c;
+    if (AMODE == kACat) {
+      seg = (c >= p.cseg[1]) + (c >= p.cseg[2]);
+      cl = c - p.cseg[seg];
+    }
+    const float* base = (seg == 0) ? p.a[0] : ((seg == 1) ? p.a[1] : p.a[2]);
+    const int ld = (seg == 0) ? p.lda[0] : ((seg == 1) ? p.lda[1] : p.lda[2]);
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int tt = a_t[i] + off;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (kin && tt >= 0 && tt < p.T) {
+        const long row = (long)a_m[i] + off;
+        if (AMODE == kACat) {
+          v = *reinterpret_cast<const f32x4*>(base + row * ld + cl);
+        } else {
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(p.a[0] + row * p.lda[0] + c);
+          const f32x4 x1 = *reinterpret_cast<const f32x4*>(p.a[1] + row * p.lda[1] + c);
+          v = x0 + x1;
+        }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) rb[i] = *reinterpret_cast<const f32x4*>(wrow[i] + k0);
+  };
+
+  auto store_tile = [&](int buf) {
+    float* a = As + buf * BM * LDK;
+    float* b = Bs + buf * BN * LDK;
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      *reinterpret_cast<f32x4*>(a + (srow + 32 * i) * LDK + c4) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      *reinterpret_cast<f32x4*>(b + (srow + 32 * i) * LDK + c4) = rb[i];
+  };
+
+  const int wm = wave / WN;
+  const int wn = wave - wm * WN;
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = p.Kp / BK;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile((kt + 1) * BK);
+    const float* a = As + cur * BM * LDK + (wm * TM * 32 + r32) * LDK + h * 16;
+    const float* b = Bs + cur * BN * LDK + (wn * TN * 32 + r32) * LDK + h * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f32x4*>(a + i * 32 * LDK + q * 4);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f32x4*>(b + j * 32 * LDK + q * 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane owns column (lane & 31) of each 32x32 tile and rows
+  // (r&3) + 8(r>>2) + 4h, r = 0..15 (gfx950 32x32 C/D map).
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + (wn * TN + j) * 32 + r32;
+    const float bv = p.bias ? p.bias[col] : 0.f;
+    const float sc = p.scale ? p.scale[col] : 1.f;
+    const float sh = p.scale ? p.shift[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rbase = m0 + (wm * TM + i) * 32 + 4 * h;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        if (row < p.M) {
+          float y = acc[i][j][r] + bv;
+          if (p.row_bias) y += p.row_bias[(size_t)(row / p.T) * p.N + col];
+          if (p.res) y += p.res[(size_t)row * p.ldres + col];
+          if (p.act == kActRelu) y = fmaxf(y, 0.f);
+          else if (p.act == kActTanh) y = tanhf(y);
+          if (p.scale) y = y * sc + sh;
+          p.out[(size_t)row * p.ldo + col] = y;
+        }
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN>
+void launch_tile(const ConvGemmArgs& p, hipStream_t s) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
+  const size_t lds = (size_t)2 * (BM + BN) * LDK * sizeof(float);
+  if (p.amode == kAAdd)
+    hipLaunchKernelGGL((conv_gemm_f32<WM, WN, TM, TN, kAAdd>), dim3(nwg), dim3(256), lds, s, p);
+  else
+    hipLaunchKernelGGL((conv_gemm_f32<WM, WN, TM, TN, kACat>), dim3(nwg), dim3(256), lds, s, p);
+  WSP_HIP(hipGetLastError());
+}
+
+}  // namespace
+
+int conv_gemm_tile_for(int N) { return (N % 128 == 0) ? 0 : 1; }
+
+void launch_conv_gemm(const ConvGemmArgs& p, hipStream_t s) {
+  WSP_CHECK(p.M > 0 && p.N > 0 && p.K > 0 && p.T > 0, "conv_gemm: empty shape");
+  WSP_CHECK(p.cin % 4 == 0, "conv_gemm: cin must be a multiple of 4");
+  WSP_CHECK(p.Kp % BK == 0 && p.Kp >= p.K, "conv_gemm: bad packed K");
+  WSP_CHECK(p.N % 64 == 0, "conv_gemm: N must be a multiple of 64");
+  for (int i = 0; i < 3; ++i) WSP_CHECK(p.lda[i] % 4 == 0, "conv_gemm: lda must be a multiple of 4");
+  if (p.amode == kACat) {
+    WSP_CHECK(p.cseg[0] == 0 && p.cseg[3] == p.cin, "conv_gemm: bad channel segments");
+    for (int i = 1; i < 3; ++i) WSP_CHECK(p.cseg[i] % 4 == 0, "conv_gemm: segment not float4 aligned");
+  }
+  if (conv_gemm_tile_for(p.N) == 0)
+    launch_tile<2, 2, 2, 2>(p, s);
+  else
+    launch_tile<4, 1, 1, 2>(p, s);
+}
+
+}  // namespace wsp

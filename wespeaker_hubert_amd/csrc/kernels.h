@@ -1,0 +1,95 @@
+// Launcher interfaces of the hand-written gfx950 kernels.
+#pragma once
+
+#include "common.h"
+
+namespace wsp {
+
+// ---------------------------------------------------------------------------
+// Implicit-GEMM 1-D convolution over channels-last frames (fp32 MFMA).
+//
+//   out[m][n] = epi( sum_{j<taps} sum_{c<cin} A(m + j*dil - pad, c) * W[n][j*cin + c] )
+//
+// Rows m = b*T + t index (utterance, frame); a tap that leaves [0, T) of its
+// utterance reads zero (the reference's zero padding).  A(row, c) is one of
+//   kACat : channel c taken from segment s (cseg[s] <= c < cseg[s+1]) of
+//           up to 3 row-major buffers -> torch.cat(dim=1) without a copy
+//   kAAdd : a[0][row][c] + a[1][row][c]   (Res2Net's `sp + spx[i]`)
+// epi(y) = ((y + bias[n] + row_bias[b][n] + res[m][n]) -> act) * scale[n] + shift[n]
+// ---------------------------------------------------------------------------
+enum AMode { kACat = 0, kAAdd = 1 };
+enum Act { kActNone = 0, kActRelu = 1, kActTanh = 2 };
+
+struct ConvGemmArgs {
+  const float* a[3];
+  int lda[3];
+  int cseg[4];
+  int cin, taps, dil, pad;
+  int M, T, N;
+  const float* w;  // [N][Kp] packed, Kp = round_up(taps*cin, 32), zero padded
+  int K, Kp;
+  const float* bias;      // [N] or null
+  const float* row_bias;  // [M/T][N] or null
+  const float* res;       // [M][ldres] or null
+  int ldres;
+  const float* scale;  // [N] or null (then shift ignored)
+  const float* shift;
+  float* out;
+  int ldo;
+  int act;
+  int amode;
+};
+
+// tile: 0 = 128x128 block (N % 128 == 0), 1 = 128x64 block (N % 64 == 0)
+void launch_conv_gemm(const ConvGemmArgs& p, hipStream_t s);
+int conv_gemm_tile_for(int N);
+
+// ---------------------------------------------------------------------------
+// Small row-batched linear: out[r][n] = act(bias[n] + sum_k in[r][k] * Wt[k][n])
+// followed by an optional affine (scale/shift).  Wt is [K][N] (k-major).
+// act: 0 none, 1 relu, 2 tanh, 3 sigmoid
+// ---------------------------------------------------------------------------
+struct SmallLinearArgs {
+  const float* in;
+  int ldin;
+  const float* wt;
+  const float* bias;
+  float* out;
+  int ldo;
+  int R, K, N;
+  int act;
+};
+void launch_small_linear(const SmallLinearArgs& p, hipStream_t s);
+
+// Per-utterance statistics over frames of a channels-last buffer x [B*T][ldx]:
+// mean[b][c] -> out[b*ldo + c]; if with_std: sqrt(var_unbiased + 1e-7)
+// -> out[b*ldo + std_off + c]  (pooling_layers.py TSTP / GLOB context).
+void launch_frame_stats(const float* x, int ldx, int B, int T, int C, float* out, int ldo,
+                        int with_std, int std_off, hipStream_t s);
+
+// out[m][c] = x[m][c] + h[m][c] * g[b][c]  (SE_Res2Block residual, ecapa_tdnn.py:156)
+void launch_residual_scale(const float* x, const float* h, const float* g, float* out, int B,
+                           int T, int C, hipStream_t s);
+
+// ASTP attentive statistics (pooling_layers.py:135-144): softmax over frames
+// of logits e [B*T][C], weighted mean/std of x [B*T][C] -> out [B][2C].
+void launch_astp_pool(const float* e, const float* x, int B, int T, int C, float* out,
+                      hipStream_t s);
+
+// Kaldi fbank + optional CMN.  `tables` = device copy of fbank_tables().
+constexpr int kFbankTableFloats = 1664 + 1024;
+void fbank_tables(float* host_tab);  // window, twiddles, sparse mel filters
+void launch_fbank(const void* wav, int dtype, int B, int N, int ld, float scale, float* feats,
+                  int T, int cmn, const float* tables, hipStream_t s);
+
+// Scoring helpers.
+void launch_l2_normalize(const float* x, const float* sub, float* y, int R, int D, hipStream_t s);
+void launch_cosine_pairs(const float* E, int D, const int32_t* ia, const int32_t* ib, int P,
+                         double* score, hipStream_t s);
+void asnorm_layout(int Ne, int Nc, int D, int* Ncp, int* Dp, size_t* bytes);
+void launch_asnorm_stats(const float* E, int Ne, const float* C, int Nc, int D, int top_n,
+                         double* mu, double* sd, float* ws, hipStream_t s);
+void launch_row_mean_accum(const float* x, const int32_t* group, int R, int D, double* acc,
+                           double* cnt, hipStream_t s);
+
+}  // namespace wsp

@@ -1,0 +1,537 @@
+// Speaker-model runtime: parameter intake (reference state_dict order),
+// BatchNorm folding + weight packing on the host in f64, device residency,
+// and the forward schedule of HIP kernels over a caller-provided workspace.
+//
+// ECAPA-TDNN forward = wespeaker/models/ecapa_tdnn.py:208-234, channels-last:
+//   layer1  Conv1dReluBn(F->C, k5)                        -> x1   [M][C]
+//   layerL  SE_Res2Block(dil L):  c1 (1x1) -> h1
+//           Res2 chain i=0..6: conv_k3(h1_i (+ h2_{i-1})) -> h2_i  (7 GEMMs)
+//           c3 (1x1) over cat(h2_0..6, h1_7)             -> h3   (no copy)
+//           SE: frame mean -> FC relu -> FC sigmoid -> x_{L} + h3 * g
+//   conv    1x1 over cat(x2, x3, x4) (no copy), ReLU      -> xp   [M][1536]
+//   ASTP    [GLOB: frame mean/std -> per-utterance bias]  -> tanh(W1 xp) -> W2
+//           -> online-softmax attentive mean/std          -> [B][3072]
+//   head    BN(3072) + Linear (+ bn2) folded into one GEMV -> embed [B][D]
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "model.h"
+
+namespace wsp {
+
+namespace {
+
+constexpr double kBnEps = 1e-5;
+
+struct DevBuf {
+  std::vector<void*> ptrs;
+  ~DevBuf() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  float* upload(const std::vector<float>& v) {
+    void* p = nullptr;
+    WSP_HIP(hipMalloc(&p, std::max<size_t>(v.size(), 1) * sizeof(float)));
+    ptrs.push_back(p);
+    if (!v.empty()) WSP_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice));
+    return static_cast<float*>(p);
+  }
+};
+
+struct ConvW {
+  float* w = nullptr;
+  float* bias = nullptr;
+  float* scale = nullptr;
+  float* shift = nullptr;
+  int N = 0, cin = 0, taps = 1, K = 0, Kp = 0;
+};
+
+struct LinW {  // small_linear weights, k-major
+  float* wt = nullptr;
+  float* bias = nullptr;
+  int K = 0, N = 0;
+};
+
+int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+}  // namespace
+
+struct Param {
+  std::string name;
+  std::vector<int64_t> shape;
+  std::vector<float> host;
+  bool set = false;
+  int64_t numel() const {
+    int64_t n = 1;
+    for (auto s : shape) n *= s;
+    return n;
+  }
+};
+
+struct ProfEntry {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t used = 0;
+  double flops = 0;
+};
+
+struct Model::Impl {
+  std::string arch;
+  bool ecapa = true;
+  int C = 512;
+  bool glob = false;
+  int feat_dim = 80, embed_dim = 192;
+  bool emb_bn = false, two_emb = false;
+  std::vector<Param> params;
+  std::map<std::string, int> idx;
+  bool finalized = false;
+  int device = 0;
+  DevBuf dev;
+
+  // ECAPA packed weights
+  ConvW layer1;
+  struct Block {
+    ConvW c1, c3, res2[7];
+    LinW se1, se2;
+  } blk[3];
+  ConvW conv, pool1, pool2;
+  LinW pool1_ctx;
+  LinW head;
+
+  // profiling
+  bool prof = false;
+  std::map<std::string, ProfEntry> prof_map;
+
+  void add(const std::string& n, std::vector<int64_t> shape) {
+    idx[n] = (int)params.size();
+    params.push_back(Param{n, std::move(shape), {}, false});
+  }
+  void add_bn(const std::string& p, int64_t c) {
+    add(p + ".weight", {c});
+    add(p + ".bias", {c});
+    add(p + ".running_mean", {c});
+    add(p + ".running_var", {c});
+    add(p + ".num_batches_tracked", {});
+  }
+  const std::vector<float>& P(const std::string& n) const {
+    auto it = idx.find(n);
+    WSP_CHECK(it != idx.end(), "missing parameter " + n);
+    const Param& p = params[it->second];
+    WSP_CHECK(p.set || p.numel() == 0, "parameter not set: " + n);
+    return p.host;
+  }
+
+  // eval BatchNorm as affine: y = x*scale + shift
+  void bn_affine(const std::string& p, std::vector<double>& sc, std::vector<double>& sh) const {
+    const auto& w = P(p + ".weight");
+    const auto& b = P(p + ".bias");
+    const auto& rm = P(p + ".running_mean");
+    const auto& rv = P(p + ".running_var");
+    sc.resize(w.size());
+    sh.resize(w.size());
+    for (size_t i = 0; i < w.size(); ++i) {
+      sc[i] = (double)w[i] / std::sqrt((double)rv[i] + kBnEps);
+      sh[i] = (double)b[i] - (double)rm[i] * sc[i];
+    }
+  }
+
+  // Conv1d weight [N][cin][taps] -> packed [N][Kp], k = tap*cin + c.
+  ConvW pack_conv(const std::vector<float>& w, int N, int cin, int taps, const float* bias,
+                  const std::string& bn) {
+    ConvW cw;
+    cw.N = N;
+    cw.cin = cin;
+    cw.taps = taps;
+    cw.K = cin * taps;
+    cw.Kp = round_up(cw.K, 32);
+    std::vector<float> packed((size_t)N * cw.Kp, 0.f);
+    for (int n = 0; n < N; ++n)
+      for (int c = 0; c < cin; ++c)
+        for (int j = 0; j < taps; ++j)
+          packed[(size_t)n * cw.Kp + j * cin + c] = w[((size_t)n * cin + c) * taps + j];
+    cw.w = dev.upload(packed);
+    if (bias) cw.bias = dev.upload(std::vector<float>(bias, bias + N));
+    if (!bn.empty()) {
+      std::vector<double> sc, sh;
+      bn_affine(bn, sc, sh);
+      std::vector<float> s(N), t(N);
+      for (int i = 0; i < N; ++i) {
+        s[i] = (float)sc[i];
+        t[i] = (float)sh[i];
+      }
+      cw.scale = dev.upload(s);
+      cw.shift = dev.upload(t);
+    }
+    return cw;
+  }
+
+  // Linear weight [N][K] (row-major, ldk) -> k-major [K][N]
+  LinW pack_lin(const float* w, int N, int K, int ldk, const float* bias) {
+    LinW lw;
+    lw.N = N;
+    lw.K = K;
+    std::vector<float> t((size_t)K * N);
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < K; ++k) t[(size_t)k * N + n] = w[(size_t)n * ldk + k];
+    lw.wt = dev.upload(t);
+    if (bias) lw.bias = dev.upload(std::vector<float>(bias, bias + N));
+    return lw;
+  }
+
+  void build_ecapa_params() {
+    const int64_t C = this->C, w = C / 8;
+    add("layer1.conv.weight", {C, feat_dim, 5});
+    add("layer1.conv.bias", {C});
+    add_bn("layer1.bn", C);
+    for (int li = 2; li <= 4; ++li) {
+      const std::string p = "layer" + std::to_string(li) + ".se_res2block";
+      add(p + ".0.conv.weight", {C, C, 1});
+      add(p + ".0.conv.bias", {C});
+      add_bn(p + ".0.bn", C);
+      for (int i = 0; i < 7; ++i) {
+        add(p + ".1.convs." + std::to_string(i) + ".weight", {w, w, 3});
+        add(p + ".1.convs." + std::to_string(i) + ".bias", {w});
+      }
+      for (int i = 0; i < 7; ++i) add_bn(p + ".1.bns." + std::to_string(i), w);
+      add(p + ".2.conv.weight", {C, C, 1});
+      add(p + ".2.conv.bias", {C});
+      add_bn(p + ".2.bn", C);
+      add(p + ".3.linear1.weight", {128, C});
+      add(p + ".3.linear1.bias", {128});
+      add(p + ".3.linear2.weight", {C, 128});
+      add(p + ".3.linear2.bias", {C});
+    }
+    add("conv.weight", {1536, 3 * C, 1});
+    add("conv.bias", {1536});
+    add("pool.linear1.weight", {128, glob ? 4608 : 1536, 1});
+    add("pool.linear1.bias", {128});
+    add("pool.linear2.weight", {1536, 128, 1});
+    add("pool.linear2.bias", {1536});
+    add_bn("bn", 3072);
+    add("linear.weight", {embed_dim, 3072});
+    add("linear.bias", {embed_dim});
+    if (emb_bn) add_bn("bn2", embed_dim);
+  }
+
+  void finalize_ecapa() {
+    const int w = C / 8;
+    layer1 = pack_conv(P("layer1.conv.weight"), C, feat_dim, 5, P("layer1.conv.bias").data(), "layer1.bn");
+    for (int li = 0; li < 3; ++li) {
+      const std::string p = "layer" + std::to_string(li + 2) + ".se_res2block";
+      Block& b = blk[li];
+      b.c1 = pack_conv(P(p + ".0.conv.weight"), C, C, 1, P(p + ".0.conv.bias").data(), p + ".0.bn");
+      for (int i = 0; i < 7; ++i) {
+        const std::string ci = p + ".1.convs." + std::to_string(i);
+        b.res2[i] = pack_conv(P(ci + ".weight"), w, w, 3, P(ci + ".bias").data(),
+                              p + ".1.bns." + std::to_string(i));
+      }
+      b.c3 = pack_conv(P(p + ".2.conv.weight"), C, C, 1, P(p + ".2.conv.bias").data(), p + ".2.bn");
+      b.se1 = pack_lin(P(p + ".3.linear1.weight").data(), 128, C, C, P(p + ".3.linear1.bias").data());
+      b.se2 = pack_lin(P(p + ".3.linear2.weight").data(), C, 128, 128, P(p + ".3.linear2.bias").data());
+    }
+    conv = pack_conv(P("conv.weight"), 1536, 3 * C, 1, P("conv.bias").data(), "");
+    const auto& l1 = P("pool.linear1.weight");
+    const int l1k = glob ? 4608 : 1536;
+    {
+      std::vector<float> wx((size_t)128 * 1536);
+      for (int n = 0; n < 128; ++n)
+        for (int k = 0; k < 1536; ++k) wx[(size_t)n * 1536 + k] = l1[(size_t)n * l1k + k];
+      pool1 = pack_conv(wx, 128, 1536, 1, P("pool.linear1.bias").data(), "");
+      if (glob) {
+        // columns 1536..4607 multiply the (constant over T) mean/std context:
+        // folded into a per-utterance bias computed by small_linear.
+        pool1_ctx = pack_lin(l1.data() + 1536, 128, 3072, l1k, P("pool.linear1.bias").data());
+      }
+    }
+    pool2 = pack_conv(P("pool.linear2.weight"), 1536, 128, 1, P("pool.linear2.bias").data(), "");
+    // head: y = Linear(BN(p)) [-> bn2] folded to y = W' p + b'
+    {
+      std::vector<double> s, t;
+      bn_affine("bn", s, t);
+      const auto& W = P("linear.weight");
+      const auto& bb = P("linear.bias");
+      const int D = embed_dim;
+      std::vector<double> s2(D, 1.0), t2(D, 0.0);
+      if (emb_bn) bn_affine("bn2", s2, t2);
+      std::vector<float> wf((size_t)D * 3072), bf(D);
+      for (int n = 0; n < D; ++n) {
+        double acc = bb[n];
+        for (int k = 0; k < 3072; ++k) {
+          const double wv = W[(size_t)n * 3072 + k];
+          wf[(size_t)n * 3072 + k] = (float)(s2[n] * wv * s[k]);
+          acc += wv * t[k];
+        }
+        bf[n] = (float)(s2[n] * acc + t2[n]);
+      }
+      head = pack_lin(wf.data(), D, 3072, 3072, bf.data());
+    }
+  }
+
+  // --------------------------------------------------------------- launch --
+  template <typename F>
+  void run(const char* tag, double flops, hipStream_t s, F&& f) {
+    if (!prof) {
+      f();
+      return;
+    }
+    ProfEntry& e = prof_map[tag];
+    if (e.used == e.ev.size()) {
+      hipEvent_t a, b;
+      WSP_HIP(hipEventCreate(&a));
+      WSP_HIP(hipEventCreate(&b));
+      e.ev.emplace_back(a, b);
+    }
+    auto& pr = e.ev[e.used++];
+    e.flops = flops;
+    WSP_HIP(hipEventRecord(pr.first, s));
+    f();
+    WSP_HIP(hipEventRecord(pr.second, s));
+  }
+
+  void gemm(const char* tag, const ConvW& cw, const float* a0, int lda, float* out, int ldo, int M,
+            int T, int dil, int pad, int act, hipStream_t s, const float* row_bias = nullptr,
+            bool use_bias = true) {
+    ConvGemmArgs g{};
+    g.a[0] = g.a[1] = g.a[2] = a0;
+    g.lda[0] = g.lda[1] = g.lda[2] = lda;
+    g.cseg[0] = 0;
+    g.cseg[1] = g.cseg[2] = g.cseg[3] = cw.cin;
+    fill(g, cw, M, T, dil, pad, out, ldo, act, row_bias, use_bias);
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm(g, s); });
+  }
+  void fill(ConvGemmArgs& g, const ConvW& cw, int M, int T, int dil, int pad, float* out, int ldo,
+            int act, const float* row_bias, bool use_bias) {
+    g.cin = cw.cin;
+    g.taps = cw.taps;
+    g.dil = dil;
+    g.pad = pad;
+    g.M = M;
+    g.T = T;
+    g.N = cw.N;
+    g.w = cw.w;
+    g.K = cw.K;
+    g.Kp = cw.Kp;
+    g.bias = use_bias ? cw.bias : nullptr;
+    g.row_bias = row_bias;
+    g.scale = cw.scale;
+    g.shift = cw.shift;
+    g.out = out;
+    g.ldo = ldo;
+    g.act = act;
+  }
+
+  size_t ecapa_ws_floats(int B, int T, size_t* offs) const {
+    const size_t M = (size_t)B * T;
+    const size_t sizes[] = {M * C, M * C, M * C, M * C,           // x1..x4
+                            M * C, M * C, M * C,                   // h1..h3
+                            (size_t)B * C, (size_t)B * 128, (size_t)B * C,  // gmean, ghid, gate
+                            M * 1536, M * 128, M * 1536,           // xp, att, logit
+                            (size_t)B * 3072, (size_t)B * 128, (size_t)B * 3072};  // gstats, rowb, pooled
+    size_t o = 0;
+    for (int i = 0; i < 16; ++i) {
+      if (offs) offs[i] = o;
+      o += (sizes[i] + 63) / 64 * 64;  // 256-B alignment
+    }
+    return o;
+  }
+
+  void forward_ecapa(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
+    const int M = B * T, w = C / 8;
+    size_t off[16];
+    ecapa_ws_floats(B, T, off);
+    float* x[5] = {nullptr, ws + off[0], ws + off[1], ws + off[2], ws + off[3]};
+    float* h1 = ws + off[4];
+    float* h2 = ws + off[5];
+    float* h3 = ws + off[6];
+    float* gmean = ws + off[7];
+    float* ghid = ws + off[8];
+    float* gate = ws + off[9];
+    float* xp = ws + off[10];
+    float* att = ws + off[11];
+    float* logit = ws + off[12];
+    float* gstats = ws + off[13];
+    float* rowb = ws + off[14];
+    float* pooled = ws + off[15];
+
+    gemm("layer1", layer1, feats, feat_dim, x[1], C, M, T, 1, 2, kActRelu, s);
+    for (int li = 0; li < 3; ++li) {
+      const Block& b = blk[li];
+      const int dil = li + 2;
+      const float* xin = x[li + 1];
+      gemm("conv1x1_CxC", b.c1, xin, C, h1, C, M, T, 1, 0, kActRelu, s);
+      for (int i = 0; i < 7; ++i) {
+        ConvGemmArgs g{};
+        if (i == 0) {
+          g.amode = kACat;
+          g.a[0] = g.a[1] = g.a[2] = h1;
+          g.lda[0] = g.lda[1] = g.lda[2] = C;
+          g.cseg[0] = 0;
+          g.cseg[1] = g.cseg[2] = g.cseg[3] = w;
+        } else {
+          g.amode = kAAdd;
+          g.a[0] = h1 + i * w;
+          g.a[1] = h2 + (i - 1) * w;
+          g.a[2] = h1;
+          g.lda[0] = g.lda[1] = g.lda[2] = C;
+        }
+        fill(g, b.res2[i], M, T, dil, dil, h2 + i * w, C, kActRelu, nullptr, true);
+        run("res2_k3", 2.0 * M * w * 3 * w, s, [&] { launch_conv_gemm(g, s); });
+      }
+      {
+        ConvGemmArgs g{};
+        g.amode = kACat;
+        g.a[0] = h2;
+        g.a[1] = h1 + 7 * w;
+        g.a[2] = h1;
+        g.lda[0] = g.lda[1] = g.lda[2] = C;
+        g.cseg[0] = 0;
+        g.cseg[1] = 7 * w;
+        g.cseg[2] = g.cseg[3] = C;
+        fill(g, b.c3, M, T, 1, 0, h3, C, kActRelu, nullptr, true);
+        run("conv1x1_CxC", 2.0 * M * C * C, s, [&] { launch_conv_gemm(g, s); });
+      }
+      run("se", 0, s, [&] {
+        launch_frame_stats(h3, C, B, T, C, gmean, C, 0, 0, s);
+        launch_small_linear({gmean, C, b.se1.wt, b.se1.bias, ghid, 128, B, C, 128, 1}, s);
+        launch_small_linear({ghid, 128, b.se2.wt, b.se2.bias, gate, C, B, 128, C, 3}, s);
+        launch_residual_scale(xin, h3, gate, x[li + 2], B, T, C, s);
+      });
+    }
+    {
+      ConvGemmArgs g{};
+      g.amode = kACat;
+      g.a[0] = x[2];
+      g.a[1] = x[3];
+      g.a[2] = x[4];
+      g.lda[0] = g.lda[1] = g.lda[2] = C;
+      g.cseg[0] = 0;
+      g.cseg[1] = C;
+      g.cseg[2] = 2 * C;
+      g.cseg[3] = 3 * C;
+      fill(g, conv, M, T, 1, 0, xp, 1536, kActRelu, nullptr, true);
+      run("conv_cat", 2.0 * M * 1536 * 3 * C, s, [&] { launch_conv_gemm(g, s); });
+    }
+    if (glob) {
+      run("glob_ctx", 0, s, [&] {
+        launch_frame_stats(xp, 1536, B, T, 1536, gstats, 3072, 1, 1536, s);
+        launch_small_linear({gstats, 3072, pool1_ctx.wt, pool1_ctx.bias, rowb, 128, B, 3072, 128, 0}, s);
+      });
+      gemm("pool_linear1", pool1, xp, 1536, att, 128, M, T, 1, 0, kActTanh, s, rowb, false);
+    } else {
+      gemm("pool_linear1", pool1, xp, 1536, att, 128, M, T, 1, 0, kActTanh, s);
+    }
+    gemm("pool_linear2", pool2, att, 128, logit, 1536, M, T, 1, 0, kActNone, s);
+    run("astp", 0, s, [&] { launch_astp_pool(logit, xp, B, T, 1536, pooled, s); });
+    run("head", 0, s, [&] {
+      launch_small_linear({pooled, 3072, head.wt, head.bias, embed, embed_dim, B, 3072, embed_dim, 0}, s);
+    });
+  }
+};
+
+Model::Model() : impl(new Impl) {}
+Model::~Model() {
+  for (auto& kv : impl->prof_map)
+    for (auto& e : kv.second.ev) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+  delete impl;
+}
+
+void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool emb_bn, bool two_emb) {
+  Impl& m = *impl;
+  m.arch = arch;
+  m.feat_dim = feat_dim;
+  m.embed_dim = embed_dim;
+  m.emb_bn = emb_bn;
+  m.two_emb = two_emb;
+  WSP_HIP(hipGetDevice(&m.device));
+  if (arch == "ECAPA_TDNN_c512" || arch == "ECAPA_TDNN_GLOB_c512" || arch == "ECAPA_TDNN_c1024" ||
+      arch == "ECAPA_TDNN_GLOB_c1024") {
+    m.ecapa = true;
+    m.C = (arch.find("c1024") != std::string::npos) ? 1024 : 512;
+    m.glob = arch.find("GLOB") != std::string::npos;
+    WSP_CHECK(feat_dim > 0 && feat_dim % 4 == 0, "ECAPA feat_dim must be a positive multiple of 4");
+    WSP_CHECK(embed_dim > 0, "embed_dim must be positive");
+    m.build_ecapa_params();
+  } else {
+    throw InvalidArg{"unsupported arch " + arch};
+  }
+}
+
+int Model::num_params() const { return (int)impl->params.size(); }
+
+void Model::param_info(int i, const char** name, int* ndim, int64_t* shape) const {
+  WSP_CHECK(i >= 0 && i < num_params(), "param index out of range");
+  const Param& p = impl->params[i];
+  *name = p.name.c_str();
+  *ndim = (int)p.shape.size();
+  for (size_t d = 0; d < p.shape.size() && d < 4; ++d) shape[d] = p.shape[d];
+}
+
+void Model::set_param(int i, const float* data, int64_t numel) {
+  WSP_CHECK(i >= 0 && i < num_params(), "param index out of range");
+  Param& p = impl->params[i];
+  WSP_CHECK(numel == p.numel(), "numel mismatch for " + p.name);
+  p.host.assign(data, data + numel);
+  p.set = true;
+}
+
+void Model::finalize() {
+  Impl& m = *impl;
+  WSP_CHECK(!m.finalized, "model already finalized");
+  int dev = 0;
+  WSP_HIP(hipGetDevice(&dev));
+  WSP_CHECK(dev == m.device, "finalize on a different device than create");
+  for (auto& p : m.params)
+    WSP_CHECK(p.set || p.name.find("num_batches_tracked") != std::string::npos,
+              "parameter not set: " + p.name);
+  m.finalize_ecapa();
+  for (auto& p : m.params) std::vector<float>().swap(p.host);
+  m.finalized = true;
+}
+
+int Model::embed_dim() const { return impl->embed_dim; }
+int Model::feat_dim() const { return impl->feat_dim; }
+
+size_t Model::workspace_bytes(int B, int T) const {
+  return impl->ecapa_ws_floats(B, T, nullptr) * sizeof(float) + 256;
+}
+
+void Model::forward(const float* feats, int B, int T, float* embed, void* ws, size_t ws_bytes,
+                    hipStream_t s) {
+  Impl& m = *impl;
+  WSP_CHECK(m.finalized, "forward before finalize");
+  WSP_CHECK(B > 0 && T > 1, "forward needs B >= 1 and T >= 2 frames");
+  WSP_CHECK((size_t)B * T < (1u << 31), "B*T too large");
+  WSP_CHECK(ws_bytes >= workspace_bytes(B, T), "workspace too small");
+  float* wsf = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+  m.forward_ecapa(feats, B, T, embed, wsf, s);
+}
+
+void Model::profile(bool on) { impl->prof = on; }
+
+void Model::profile_query(const std::string& tag, int* launches, double* total_ms, double* flops) {
+  auto it = impl->prof_map.find(tag);
+  *launches = 0;
+  *total_ms = 0;
+  *flops = 0;
+  if (it == impl->prof_map.end()) return;
+  ProfEntry& e = it->second;
+  for (size_t i = 0; i < e.used; ++i) {
+    WSP_HIP(hipEventSynchronize(e.ev[i].second));
+    float ms = 0;
+    WSP_HIP(hipEventElapsedTime(&ms, e.ev[i].first, e.ev[i].second));
+    *total_ms += ms;
+  }
+  *launches = (int)e.used;
+  *flops = e.flops;
+  e.used = 0;
+}
+
+}  // namespace wsp

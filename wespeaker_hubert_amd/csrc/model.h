@@ -1,0 +1,34 @@
+// Speaker model runtime object behind the wsp_model_* C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+namespace wsp {
+
+class Model {
+ public:
+  Model();
+  ~Model();
+  void create(const std::string& arch, int feat_dim, int embed_dim, bool emb_bn, bool two_emb);
+  int num_params() const;
+  void param_info(int i, const char** name, int* ndim, int64_t* shape) const;
+  void set_param(int i, const float* data, int64_t numel);
+  void finalize();
+  int embed_dim() const;
+  int feat_dim() const;
+  size_t workspace_bytes(int B, int T) const;
+  void forward(const float* feats, int B, int T, float* embed, void* ws, size_t ws_bytes,
+               hipStream_t s);
+  void profile(bool on);
+  void profile_query(const std::string& tag, int* launches, double* total_ms, double* flops);
+
+  struct Impl;
+
+ private:
+  Impl* impl;
+};
+
+}  // namespace wsp

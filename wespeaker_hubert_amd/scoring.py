@@ -1,0 +1,185 @@
+"""Cosine / AS-Norm scoring on the GPU, plus the reference's score-file formats.
+
+Mirrors wespeaker/bin/score.py (trials_cosine_score, calculate_mean_from_kaldi_vec),
+wespeaker/bin/score_norm.py (get_mean_std, AS-Norm / S-Norm main),
+tools/vector_mean.py (compute_vector_mean) and the EER/minDCF metrics of
+wespeaker/utils/score_metrics.py used by bin/compute_metrics.py.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _stream(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def l2_normalize(x: torch.Tensor, sub: Optional[torch.Tensor] = None) -> torch.Tensor:
+    x = x.float().contiguous()
+    y = torch.empty_like(x)
+    R, D = x.shape
+    subp = sub.float().contiguous().data_ptr() if sub is not None else None
+    _lib.check(_lib.load().wsp_l2_normalize(x.data_ptr(), subp, y.data_ptr(), R, D, _stream(x)),
+               "wsp_l2_normalize")
+    return y
+
+
+def asnorm_stats(emb: torch.Tensor, cohort: torch.Tensor, top_n: int,
+                 mean_vec: Optional[torch.Tensor] = None) -> Tuple[np.ndarray, np.ndarray]:
+    """get_mean_std (score_norm.py:26-36) on (emb - mean_vec), (cohort - mean_vec)."""
+    e = l2_normalize(emb, mean_vec)
+    c = l2_normalize(cohort, mean_vec)
+    Ne, D = e.shape
+    Nc = c.shape[0]
+    if not 1 <= top_n <= Nc:
+        raise ValueError(f"top_n={top_n} outside [1, {Nc}]")
+    nbytes = ctypes.c_size_t()
+    _lib.check(_lib.load().wsp_asnorm_workspace_bytes(Ne, Nc, D, ctypes.byref(nbytes)), "asnorm ws")
+    ws = torch.empty(nbytes.value, dtype=torch.uint8, device=e.device)
+    mu = torch.empty(Ne, dtype=torch.float64, device=e.device)
+    sd = torch.empty(Ne, dtype=torch.float64, device=e.device)
+    _lib.check(_lib.load().wsp_asnorm_stats(e.data_ptr(), Ne, c.data_ptr(), Nc, D, int(top_n), mu.data_ptr(),
+                                            sd.data_ptr(), ws.data_ptr(), ws.numel(), _stream(e)),
+               "wsp_asnorm_stats")
+    return mu.cpu().numpy(), sd.cpu().numpy()
+
+
+def cosine_pairs(E: torch.Tensor, idx_a, idx_b) -> np.ndarray:
+    E = E.float().contiguous()
+    ia = torch.as_tensor(np.asarray(idx_a, dtype=np.int32), device=E.device)
+    ib = torch.as_tensor(np.asarray(idx_b, dtype=np.int32), device=E.device)
+    out = torch.empty(ia.numel(), dtype=torch.float64, device=E.device)
+    _lib.check(_lib.load().wsp_cosine_pairs(E.data_ptr(), E.shape[1], ia.data_ptr(), ib.data_ptr(), ia.numel(),
+                                            out.data_ptr(), _stream(E)), "wsp_cosine_pairs")
+    return out.cpu().numpy()
+
+
+def group_sums(x: torch.Tensor, groups, n_groups: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    x = x.float().contiguous()
+    g = torch.as_tensor(np.asarray(groups, dtype=np.int32), device=x.device)
+    acc = torch.zeros(n_groups, x.shape[1], dtype=torch.float64, device=x.device)
+    cnt = torch.zeros(n_groups, dtype=torch.float64, device=x.device)
+    _lib.check(_lib.load().wsp_row_mean_accum(x.data_ptr(), g.data_ptr(), x.shape[0], x.shape[1],
+                                              acc.data_ptr(), cnt.data_ptr(), _stream(x)), "wsp_row_mean_accum")
+    return acc, cnt
+
+
+def group_means(x: torch.Tensor, groups, n_groups: int) -> np.ndarray:
+    acc, cnt = group_sums(x, groups, n_groups)
+    return (acc / cnt.clamp(min=1).unsqueeze(1)).cpu().numpy()
+
+
+# ------------------------------------------------------------- metrics ---
+def compute_pmiss_pfa_rbst(scores, labels, weights=None):
+    """score_metrics.py:58-76."""
+    idx = np.argsort(scores)
+    labels = np.asarray(labels)[idx]
+    weights = np.ones(labels.shape, dtype="f8") if weights is None else np.asarray(weights)[idx]
+    tgt = weights * (labels == 1).astype("f8")
+    imp = weights * (labels == 0).astype("f8")
+    return np.cumsum(tgt) / np.sum(tgt), 1 - np.cumsum(imp) / np.sum(imp)
+
+
+def compute_eer(fnr, fpr, scores=None):
+    """score_metrics.py:79-93."""
+    d = fnr - fpr
+    x1 = np.flatnonzero(d >= 0)[0]
+    x2 = np.flatnonzero(d < 0)[-1]
+    a = (fnr[x1] - fpr[x1]) / (fpr[x2] - fpr[x1] - (fnr[x2] - fnr[x1]))
+    eer = fnr[x1] + a * (fnr[x2] - fnr[x1])
+    if scores is not None:
+        return eer, np.sort(scores)[x1]
+    return eer
+
+
+def compute_c_norm(fnr, fpr, p_target, c_miss=1, c_fa=1):
+    """score_metrics.py:96-105."""
+    c_det = min(c_miss * fnr * p_target + c_fa * fpr * (1 - p_target))
+    return c_det / min(c_miss * p_target, c_fa * (1 - p_target))
+
+
+# --------------------------------------------------------- file drivers ---
+def read_trials(path: str) -> List[List[str]]:
+    with open(path, "r", encoding="utf8") as f:
+        return [ln.strip().split() for ln in f if ln.strip()]
+
+
+def trials_cosine_score(emb: Dict[str, np.ndarray], trials: Sequence[str], store_dir: str,
+                        mean_vec: Optional[np.ndarray] = None, device: str = "cuda") -> List[str]:
+    """bin/score.py:38-72 on the GPU; writes `<trial>.score` with `{:.5f}` scores."""
+    keys = list(emb.keys())
+    kidx = {k: i for i, k in enumerate(keys)}
+    E = torch.from_numpy(np.stack([emb[k] for k in keys]).astype(np.float32)).to(device)
+    if mean_vec is not None:
+        E = E - torch.from_numpy(np.asarray(mean_vec, dtype=np.float32)).to(device)
+    out_paths = []
+    os.makedirs(store_dir, exist_ok=True)
+    for trial in trials:
+        lines = read_trials(trial)
+        ia = [kidx[s[0]] for s in lines]
+        ib = [kidx[s[1]] for s in lines]
+        sc = cosine_pairs(E, ia, ib)
+        path = os.path.join(store_dir, os.path.basename(trial) + ".score")
+        with open(path, "w") as w:
+            for s, v in zip(lines, sc):
+                if len(s) == 3:
+                    w.write("{} {} {:.5f} {}\n".format(s[0], s[1], v, s[2]))
+                else:
+                    w.write("{} {} {:.5f}\n".format(s[0], s[1], v))
+        out_paths.append(path)
+    return out_paths
+
+
+def score_norm(score_norm_method: str, top_n: int, trial_score_file: str, score_norm_file: str,
+               cohort: Dict[str, np.ndarray], eval_emb: Dict[str, np.ndarray],
+               mean_vec: Optional[np.ndarray] = None, device: str = "cuda") -> None:
+    """bin/score_norm.py:54-115 (asnorm / snorm) with the statistics on the GPU."""
+    rows = read_trials(trial_score_file)
+    enroll = sorted(set(r[0] for r in rows))
+    test = sorted(set(r[1] for r in rows))
+    mv = np.zeros(next(iter(eval_emb.values())).shape, np.float32) if mean_vec is None else \
+        np.asarray(mean_vec, np.float32)
+    ckeys = list(cohort.keys())
+    C = torch.from_numpy(np.stack([cohort[k] for k in ckeys]).astype(np.float32)).to(device)
+    if score_norm_method == "snorm":
+        top_n = C.shape[0]
+    elif score_norm_method != "asnorm":
+        raise ValueError(score_norm_method)
+    mvt = torch.from_numpy(mv).to(device)
+    Ee = np.stack([eval_emb[k] for k in enroll]).astype(np.float32)
+    Et = np.stack([eval_emb[k] for k in test]).astype(np.float32)
+    e_mu, e_sd = asnorm_stats(torch.from_numpy(Ee).to(device), C, top_n, mvt)
+    t_mu, t_sd = asnorm_stats(torch.from_numpy(Et).to(device), C, top_n, mvt)
+    ei = {k: i for i, k in enumerate(enroll)}
+    ti = {k: i for i, k in enumerate(test)}
+    e_mag = np.linalg.norm(Ee - mv, axis=1)
+    t_mag = np.linalg.norm(Et - mv, axis=1)
+    with open(score_norm_file, "w", encoding="utf-8") as fout:
+        for r in rows:
+            a, b = ei[r[0]], ti[r[1]]
+            s = float(r[2])
+            ns = 0.5 * ((s - e_mu[a]) / e_sd[a] + (s - t_mu[b]) / t_sd[b])
+            fout.write("{} {} {:.5f} {} {:.4f} {:.4f} {:.4f} {:.4f}\n".format(
+                r[0], r[1], ns, r[3], e_mag[a], t_mag[b], e_mu[a], t_mu[b]))
+
+
+def compute_metrics(scores_file: str, p_target=0.01, c_miss=1, c_fa=1) -> Tuple[float, float]:
+    """bin/compute_metrics.py:25-50 -> (EER %, minDCF)."""
+    scores, labels = [], []
+    with open(scores_file) as f:
+        for line in f:
+            tok = line.strip().split()
+            scores.append(float(tok[2]))
+            labels.append(tok[3] == "target")
+    scores = np.hstack(scores)
+    labels = np.hstack(labels)
+    fnr, fpr = compute_pmiss_pfa_rbst(scores, labels)
+    eer, _ = compute_eer(fnr, fpr, scores)
+    return 100 * eer, compute_c_norm(fnr, fpr, p_target, c_miss, c_fa)
