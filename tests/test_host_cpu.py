@@ -1,0 +1,42 @@
+"""Host-side logic that needs no GPU: registry, state_dict intake, errors."""
+import numpy as np
+import pytest
+import torch
+
+from wespeaker_hubert_amd import arch as A
+from wespeaker_hubert_amd.speaker_model import HipSpeakerModel, get_speaker_model
+from wespeaker_hubert_amd.synthetic import synth_state_dict
+
+
+def test_load_state_dict_accepts_reference_layout_and_reports_extras(caplog):
+    m = get_speaker_model("ECAPA_TDNN_GLOB_c512")(feat_dim=80, embed_dim=192)
+    sd = synth_state_dict(0, m.state_dict_layout())
+    sd = {k: torch.from_numpy(v) for k, v in sd.items()}
+    sd["projection.weight"] = torch.zeros(10, 192)   # training-only head in avg_model.pt
+    del sd["linear.bias"]
+    missing, unexpected = m.load_state_dict(sd)
+    assert missing == ["linear.bias"]
+    assert unexpected == ["projection.weight"]
+    assert "missing tensor: linear.bias" in caplog.text
+
+
+def test_shape_mismatch_raises():
+    m = HipSpeakerModel("ECAPA_TDNN_c512", feat_dim=80, embed_dim=192)
+    with pytest.raises(ValueError):
+        m.load_state_dict({"layer1.conv.weight": np.zeros((512, 80, 3), np.float32)})
+
+
+def test_unknown_model_name():
+    with pytest.raises(KeyError):
+        get_speaker_model("NOPE_c1")
+
+
+def test_cpu_device_is_refused():
+    m = HipSpeakerModel("ECAPA_TDNN_c512", feat_dim=80, embed_dim=192)
+    with pytest.raises(RuntimeError):
+        m.to("cpu")
+
+
+def test_flop_count_c1024():
+    spec = A.make_spec("ECAPA_TDNN_c1024", feat_dim=80, embed_dim=192)
+    assert abs(A.ecapa_gflop_per_utt(spec, 498) - 12.80) < 0.05

@@ -25,7 +25,8 @@ logger = logging.getLogger(__name__)
 def _to_numpy(v) -> np.ndarray:
     if isinstance(v, torch.Tensor):
         return v.detach().to("cpu").contiguous().numpy()
-    return np.ascontiguousarray(v)
+    a = np.asarray(v)
+    return a if a.flags.c_contiguous else a.copy()  # (ascontiguousarray turns 0-d into 1-d)
 
 
 class HipSpeakerModel:
