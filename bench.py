@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--precision", type=int, default=1, help="1 = bf16x3 split MFMA, 0 = f32 MFMA")
+    ap.add_argument("--x3-variant", type=int, default=None)
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing pass")
     return ap.parse_args()
 
@@ -91,6 +93,9 @@ def main():
     model = HipSpeakerModel(args.arch, feat_dim=80, embed_dim=192)
     sd = synth_state_dict(1234, model.state_dict_layout())
     model.load_state_dict(sd)
+    model.set_option("precision", args.precision)
+    if args.x3_variant is not None:
+        model.set_option("x3_variant", args.x3_variant)
     model.to(dev)
 
     # inputs resident in HBM before the timed region (per-rank shard)

@@ -100,6 +100,12 @@ int wsp_model_workspace_bytes(const wsp_model* m, int B, int T, size_t* bytes);
 int wsp_model_forward(wsp_model* m, const float* feats, int B, int T, float* embed,
                       void* workspace, size_t workspace_bytes, void* stream);
 
+/* Runtime options (any time after create):
+ *   "precision"  1 = bf16x3 split MFMA (default; fp32-class accuracy),
+ *                0 = exact f32 MFMA
+ *   "x3_variant" bf16x3 block tile: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves) */
+int wsp_model_set_option(wsp_model* m, const char* key, int value);
+
 /* Per-kernel-class timing with HIP events recorded on the launch stream
  * around every launch (used by bench.py for the roofline figure). */
 int wsp_model_profile(wsp_model* m, int enable);

@@ -40,28 +40,36 @@ def _assert_emb(got, ref):
     assert _cos_rows(got, ref).min() >= EMB_COS
 
 
-def _hip_model(arch, seed, **kw):
+def _hip_model(arch, seed, precision=1, variant=0, **kw):
     from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
     m = HipSpeakerModel(arch, **kw)
+    m.set_option("precision", precision)
+    m.set_option("x3_variant", variant)
     sd = synth_state_dict(seed, m.state_dict_layout())
     m.load_state_dict(sd)
     return m.to(DEV), sd
 
 
+PREC = [(1, 0), (1, 1), (0, 0)]
+PREC_IDS = ["bf16x3", "bf16x3_256", "f32"]
+
+
+@pytest.mark.parametrize("prec", PREC, ids=PREC_IDS)
 @pytest.mark.parametrize("path", ECAPA_FIX, ids=[os.path.basename(p)[:-4] for p in ECAPA_FIX])
-def test_ecapa_matches_reference_fixture(path):
+def test_ecapa_matches_reference_fixture(path, prec):
     z = np.load(path, allow_pickle=False)
-    m, _ = _hip_model(str(z["arch"]), int(z["weight_seed"]), feat_dim=int(z["feat_dim"]),
+    m, _ = _hip_model(str(z["arch"]), int(z["weight_seed"]), prec[0], prec[1], feat_dim=int(z["feat_dim"]),
                       embed_dim=int(z["embed_dim"]), emb_bn=bool(int(z["emb_bn"])))
     x = synth_feats(int(z["input_seed"]), int(z["B"]), int(z["T"]), int(z["feat_dim"]))
     _, emb = m(torch.from_numpy(x).to(DEV))
     _assert_emb(emb.cpu().numpy(), z["embed"])
 
 
+@pytest.mark.parametrize("prec", PREC, ids=PREC_IDS)
 @pytest.mark.parametrize("arch,B,T", [("ECAPA_TDNN_c1024", 6, 498), ("ECAPA_TDNN_c512", 5, 263),
                                       ("ECAPA_TDNN_GLOB_c512", 3, 77), ("ECAPA_TDNN_GLOB_c1024", 2, 2)])
-def test_ecapa_matches_oracle_batched(arch, B, T):
-    m, sd = _hip_model(arch, 7, feat_dim=80, embed_dim=192)
+def test_ecapa_matches_oracle_batched(arch, B, T, prec):
+    m, sd = _hip_model(arch, 7, prec[0], prec[1], feat_dim=80, embed_dim=192)
     x = synth_feats(99, B, T, 80)
     _, emb = m(torch.from_numpy(x).to(DEV))
     with torch.no_grad():

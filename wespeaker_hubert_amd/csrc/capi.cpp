@@ -147,6 +147,13 @@ int wsp_model_forward(wsp_model* m, const float* feats, int B, int T, float* emb
   });
 }
 
+int wsp_model_set_option(wsp_model* m, const char* key, int value) {
+  WSP_GUARD({
+    WSP_CHECK(m && key, "null argument");
+    m->m.set_option(key, value);
+  });
+}
+
 int wsp_model_profile(wsp_model* m, int enable) {
   WSP_GUARD({
     WSP_CHECK(m, "null model");

@@ -40,6 +40,11 @@ struct ConvGemmArgs {
   int amode;
 };
 
+// bf16x3 split-precision variant (conv_gemm_x3.hip); whi/wlo = packed [N][Kp]
+// bf16 hi/lo images of W.  variant: 0 = 128x128/4 waves, 1 = 256x128/8 waves.
+void launch_conv_gemm_x3(const ConvGemmArgs& p, const void* whi, const void* wlo, int variant,
+                         hipStream_t s);
+
 // tile: 0 = 128x128 block (N % 128 == 0), 1 = 128x64 block (N % 64 == 0)
 void launch_conv_gemm(const ConvGemmArgs& p, hipStream_t s);
 int conv_gemm_tile_for(int N);

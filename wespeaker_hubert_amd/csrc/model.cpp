@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdint>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -35,6 +36,13 @@ struct DevBuf {
   ~DevBuf() {
     for (void* p : ptrs) (void)hipFree(p);
   }
+  void* upload_u16(const std::vector<uint16_t>& v) {
+    void* p = nullptr;
+    WSP_HIP(hipMalloc(&p, std::max<size_t>(v.size(), 1) * sizeof(uint16_t)));
+    ptrs.push_back(p);
+    if (!v.empty()) WSP_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    return p;
+  }
   float* upload(const std::vector<float>& v) {
     void* p = nullptr;
     WSP_HIP(hipMalloc(&p, std::max<size_t>(v.size(), 1) * sizeof(float)));
@@ -46,6 +54,8 @@ struct DevBuf {
 
 struct ConvW {
   float* w = nullptr;
+  void* whi = nullptr;  // bf16 hi / lo split images for the bf16x3 kernel
+  void* wlo = nullptr;
   float* bias = nullptr;
   float* scale = nullptr;
   float* shift = nullptr;
@@ -59,6 +69,20 @@ struct LinW {  // small_linear weights, k-major
 };
 
 int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+// fp32 -> bf16, round to nearest even (matches v_cvt_pk_bf16_f32 on finite values)
+uint16_t f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+float bf2f(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
 
 }  // namespace
 
@@ -102,6 +126,10 @@ struct Model::Impl {
   ConvW conv, pool1, pool2;
   LinW pool1_ctx;
   LinW head;
+
+  // 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA
+  int precision = 1;
+  int x3_variant = 0;
 
   // profiling
   bool prof = false;
@@ -155,6 +183,15 @@ struct Model::Impl {
         for (int j = 0; j < taps; ++j)
           packed[(size_t)n * cw.Kp + j * cin + c] = w[((size_t)n * cin + c) * taps + j];
     cw.w = dev.upload(packed);
+    {
+      std::vector<uint16_t> hi(packed.size()), lo(packed.size());
+      for (size_t i = 0; i < packed.size(); ++i) {
+        hi[i] = f2bf(packed[i]);
+        lo[i] = f2bf(packed[i] - bf2f(hi[i]));
+      }
+      cw.whi = dev.upload_u16(hi);
+      cw.wlo = dev.upload_u16(lo);
+    }
     if (bias) cw.bias = dev.upload(std::vector<float>(bias, bias + N));
     if (!bn.empty()) {
       std::vector<double> sc, sh;
@@ -302,7 +339,13 @@ struct Model::Impl {
     g.cseg[0] = 0;
     g.cseg[1] = g.cseg[2] = g.cseg[3] = cw.cin;
     fill(g, cw, M, T, dil, pad, out, ldo, act, row_bias, use_bias);
-    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm(g, s); });
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch(g, cw, s); });
+  }
+  void launch(const ConvGemmArgs& g, const ConvW& cw, hipStream_t s) {
+    if (precision == 1)
+      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant, s);
+    else
+      launch_conv_gemm(g, s);
   }
   void fill(ConvGemmArgs& g, const ConvW& cw, int M, int T, int dil, int pad, float* out, int ldo,
             int act, const float* row_bias, bool use_bias) {
@@ -380,7 +423,7 @@ struct Model::Impl {
           g.lda[0] = g.lda[1] = g.lda[2] = C;
         }
         fill(g, b.res2[i], M, T, dil, dil, h2 + i * w, C, kActRelu, nullptr, true);
-        run("res2_k3", 2.0 * M * w * 3 * w, s, [&] { launch_conv_gemm(g, s); });
+        run("res2_k3", 2.0 * M * w * 3 * w, s, [&] { launch(g, b.res2[i], s); });
       }
       {
         ConvGemmArgs g{};
@@ -393,7 +436,7 @@ struct Model::Impl {
         g.cseg[1] = 7 * w;
         g.cseg[2] = g.cseg[3] = C;
         fill(g, b.c3, M, T, 1, 0, h3, C, kActRelu, nullptr, true);
-        run("conv1x1_CxC", 2.0 * M * C * C, s, [&] { launch_conv_gemm(g, s); });
+        run("conv1x1_CxC", 2.0 * M * C * C, s, [&] { launch(g, b.c3, s); });
       }
       run("se", 0, s, [&] {
         launch_frame_stats(h3, C, B, T, C, gmean, C, 0, 0, s);
@@ -414,7 +457,7 @@ struct Model::Impl {
       g.cseg[2] = 2 * C;
       g.cseg[3] = 3 * C;
       fill(g, conv, M, T, 1, 0, xp, 1536, kActRelu, nullptr, true);
-      run("conv_cat", 2.0 * M * 1536 * 3 * C, s, [&] { launch_conv_gemm(g, s); });
+      run("conv_cat", 2.0 * M * 1536 * 3 * C, s, [&] { launch(g, conv, s); });
     }
     if (glob) {
       run("glob_ctx", 0, s, [&] {
@@ -515,6 +558,18 @@ void Model::forward(const float* feats, int B, int T, float* embed, void* ws, si
 }
 
 void Model::profile(bool on) { impl->prof = on; }
+
+void Model::set_option(const std::string& key, int value) {
+  if (key == "precision") {
+    WSP_CHECK(value == 0 || value == 1, "precision must be 0 (f32) or 1 (bf16x3)");
+    impl->precision = value;
+  } else if (key == "x3_variant") {
+    WSP_CHECK(value == 0 || value == 1, "x3_variant must be 0 or 1");
+    impl->x3_variant = value;
+  } else {
+    throw InvalidArg{"unknown option " + key};
+  }
+}
 
 void Model::profile_query(const std::string& tag, int* launches, double* total_ms, double* flops) {
   auto it = impl->prof_map.find(tag);

@@ -23,6 +23,7 @@ class Model {
   void forward(const float* feats, int B, int T, float* embed, void* ws, size_t ws_bytes,
                hipStream_t s);
   void profile(bool on);
+  void set_option(const std::string& key, int value);
   void profile_query(const std::string& tag, int* launches, double* total_ms, double* flops);
 
   struct Impl;

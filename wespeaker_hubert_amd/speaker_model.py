@@ -42,6 +42,7 @@ class HipSpeakerModel:
         self._handle: Optional[ctypes.c_void_p] = None
         self._device: Optional[int] = None
         self._ws: Optional[torch.Tensor] = None
+        self._options: Dict[str, int] = {}
 
     # ----------------------------------------------------------- weights --
     def state_dict_layout(self) -> List[Tuple[str, Tuple[int, ...]]]:
@@ -124,6 +125,8 @@ class HipSpeakerModel:
                     raise RuntimeError(f"{key}: shape {arr.shape} != {want}")
                 _lib.check(lib.wsp_model_set_param(h, i, arr.ctypes.data, arr.size), "set_param " + key)
             _lib.check(lib.wsp_model_finalize(h), "wsp_model_finalize")
+            for k, v in self._options.items():
+                _lib.check(lib.wsp_model_set_option(h, k.encode(), v), "set_option " + k)
         except Exception:
             lib.wsp_model_destroy(h)
             raise
@@ -169,6 +172,12 @@ class HipSpeakerModel:
         return None, self.embed(feats)
 
     forward = __call__
+
+    def set_option(self, key: str, value: int):
+        """'precision': 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA."""
+        self._options[key] = int(value)
+        if self._handle is not None:
+            _lib.check(_lib.load().wsp_model_set_option(self._handle, key.encode(), int(value)), "set_option")
 
     # ----------------------------------------------------------- profile --
     def profile(self, enable: bool):
