@@ -40,7 +40,7 @@ def _assert_emb(got, ref):
     assert _cos_rows(got, ref).min() >= EMB_COS
 
 
-def _hip_model(arch, seed, precision=1, variant=0, **kw):
+def _hip_model(arch, seed, precision=1, variant=1, **kw):
     from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
     m = HipSpeakerModel(arch, **kw)
     m.set_option("precision", precision)
@@ -50,8 +50,8 @@ def _hip_model(arch, seed, precision=1, variant=0, **kw):
     return m.to(DEV), sd
 
 
-PREC = [(1, 0), (1, 1), (0, 0)]
-PREC_IDS = ["bf16x3", "bf16x3_256", "f32"]
+PREC = [(1, 1), (1, 0), (0, 0)]
+PREC_IDS = ["bf16x3_256", "bf16x3_128", "f32"]
 
 
 @pytest.mark.parametrize("prec", PREC, ids=PREC_IDS)

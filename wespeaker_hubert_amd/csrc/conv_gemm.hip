@@ -17,7 +17,7 @@
 //   the same permutation on both operands (conflict-free: row stride 9 slots).
 //   Global->LDS staging is register-staged float4 (128-B row segments),
 //   issued before the MFMA block and written after it (cdna guide T14).
-#include "kernels.h"
+#include "gemm_common.h"
 
 namespace wsp {
 
@@ -26,7 +26,7 @@ namespace {
 constexpr int BK = 32;
 constexpr int LDK = BK + 4;
 
-template <int WM, int WN, int TM, int TN, int AMODE>
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI>
 __global__ __launch_bounds__(256, 2) void conv_gemm_f32(const ConvGemmArgs p) {
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
@@ -52,53 +52,19 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(const ConvGemmArgs p) {
   // ---- staging geometry: thread loads rows (tid>>3) + 32 i, k-chunk (tid&7)
   const int srow = tid >> 3;
   const int c4 = (tid & 7) * 4;
-  int a_m[AR], a_t[AR];
+  ALoader<AR, AMODE, UNI> al;
+  al.init(p, m0, srow, 32, c4);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w);
+  int woff[BR];
 #pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int m = m0 + srow + 32 * i;
-    a_m[i] = m;
-    a_t[i] = (m < p.M) ? (m % p.T) : -0x40000000;  // invalid rows never pass the t-range test
-  }
-  const float* wrow[BR];
-#pragma unroll
-  for (int i = 0; i < BR; ++i) wrow[i] = p.w + (size_t)(n0 + srow + 32 * i) * p.Kp + c4;
+  for (int i = 0; i < BR; ++i) woff[i] = ((n0 + srow + 32 * i) * p.Kp + c4) * 4;
 
   f32x4 ra[AR], rb[BR];
 
   auto load_tile = [&](int k0) {
-    const int k = k0 + c4;
-    int j = 0, c = 0;
-    bool kin = k < p.K;
-    if (kin) {
-      j = k / p.cin;
-      c = k - j * p.cin;
-    }
-    const int off = j * p.dil - p.pad;
-    int seg = 0, cl = c;
-    if (AMODE == kACat) {
-      seg = (c >= p.cseg[1]) + (c >= p.cseg[2]);
-      cl = c - p.cseg[seg];
-    }
-    const float* base = (seg == 0) ? p.a[0] : ((seg == 1) ? p.a[1] : p.a[2]);
-    const int ld = (seg == 0) ? p.lda[0] : ((seg == 1) ? p.lda[1] : p.lda[2]);
 #pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int tt = a_t[i] + off;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (kin && tt >= 0 && tt < p.T) {
-        const long row = (long)a_m[i] + off;
-        if (AMODE == kACat) {
-          v = *reinterpret_cast<const f32x4*>(base + row * ld + cl);
-        } else {
-          const f32x4 x0 = *reinterpret_cast<const f32x4*>(p.a[0] + row * p.lda[0] + c);
-          const f32x4 x1 = *reinterpret_cast<const f32x4*>(p.a[1] + row * p.lda[1] + c);
-          v = x0 + x1;
-        }
-      }
-      ra[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) rb[i] = *reinterpret_cast<const f32x4*>(wrow[i] + k0);
+    for (int i = 0; i < BR; ++i) rb[i] = bload4(rw, woff[i] + k0 * 4);
+    al.load(k0, ra);
   };
 
   auto store_tile = [&](int buf) {
@@ -182,16 +148,25 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(const ConvGemmArgs p) {
   }
 }
 
-template <int WM, int WN, int TM, int TN>
-void launch_tile(const ConvGemmArgs& p, hipStream_t s) {
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI>
+void launch_k(const ConvGemmArgs& p, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const size_t lds = (size_t)2 * (BM + BN) * LDK * sizeof(float);
-  if (p.amode == kAAdd)
-    hipLaunchKernelGGL((conv_gemm_f32<WM, WN, TM, TN, kAAdd>), dim3(nwg), dim3(256), lds, s, p);
-  else
-    hipLaunchKernelGGL((conv_gemm_f32<WM, WN, TM, TN, kACat>), dim3(nwg), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((conv_gemm_f32<WM, WN, TM, TN, AMODE, UNI>), dim3(nwg), dim3(256), lds, s, p);
   WSP_HIP(hipGetLastError());
+}
+
+template <int WM, int WN, int TM, int TN>
+void launch_tile(const ConvGemmArgs& p, hipStream_t s) {
+  const bool uni = uniform_ktiles(p);
+  if (p.amode == kAAdd) {
+    if (uni) launch_k<WM, WN, TM, TN, kAAdd, true>(p, s);
+    else launch_k<WM, WN, TM, TN, kAAdd, false>(p, s);
+  } else {
+    if (uni) launch_k<WM, WN, TM, TN, kACat, true>(p, s);
+    else launch_k<WM, WN, TM, TN, kACat, false>(p, s);
+  }
 }
 
 }  // namespace
@@ -199,15 +174,7 @@ void launch_tile(const ConvGemmArgs& p, hipStream_t s) {
 int conv_gemm_tile_for(int N) { return (N % 128 == 0) ? 0 : 1; }
 
 void launch_conv_gemm(const ConvGemmArgs& p, hipStream_t s) {
-  WSP_CHECK(p.M > 0 && p.N > 0 && p.K > 0 && p.T > 0, "conv_gemm: empty shape");
-  WSP_CHECK(p.cin % 4 == 0, "conv_gemm: cin must be a multiple of 4");
-  WSP_CHECK(p.Kp % BK == 0 && p.Kp >= p.K, "conv_gemm: bad packed K");
-  WSP_CHECK(p.N % 64 == 0, "conv_gemm: N must be a multiple of 64");
-  for (int i = 0; i < 3; ++i) WSP_CHECK(p.lda[i] % 4 == 0, "conv_gemm: lda must be a multiple of 4");
-  if (p.amode == kACat) {
-    WSP_CHECK(p.cseg[0] == 0 && p.cseg[3] == p.cin, "conv_gemm: bad channel segments");
-    for (int i = 1; i < 3; ++i) WSP_CHECK(p.cseg[i] % 4 == 0, "conv_gemm: segment not float4 aligned");
-  }
+  check_conv_args(p, "conv_gemm");
   if (conv_gemm_tile_for(p.N) == 0)
     launch_tile<2, 2, 2, 2>(p, s);
   else

@@ -15,7 +15,7 @@
 // hi/lo bf16 while staging; W is pre-split on the host.  LDS rows are
 // 32 bf16 + 8 pad (80 B): the 16-byte fragment reads (row = lane&31,
 // k = 16 s + 8 (lane>>5)) hit 16 distinct slots per ds_read_b128 group.
-#include "kernels.h"
+#include "gemm_common.h"
 
 namespace wsp {
 
@@ -27,7 +27,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int BK = 32;
 constexpr int ROWB = 80;  // bytes per LDS row (32 bf16 + 8 pad)
 
-template <int WM, int WN, int TM, int TN, int AMODE>
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE>
 __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArgs p,
                                                                const __bf16* __restrict__ whi,
                                                                const __bf16* __restrict__ wlo) {
@@ -39,7 +39,8 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   constexpr int ROWS_A = NT / 8;        // A rows covered per pass
   constexpr int A_BYTES = BM * ROWB;    // one bf16 image (hi or lo) of the A tile
   constexpr int B_BYTES = BN * ROWB;
-  constexpr int STAGE = 2 * A_BYTES + 2 * B_BYTES;
+  constexpr int B_LO = B_BYTES + 64;  // lo image skewed by 16 banks vs hi (conflict-free stores)
+  constexpr int STAGE = 2 * A_BYTES + B_LO + B_BYTES;
   static_assert(AR >= 1 && BR >= 1, "tile too small for the thread count");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -58,62 +59,39 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   // ---- A staging geometry
   const int srow = tid >> 3;
   const int c4 = (tid & 7) * 4;
-  int a_m[AR], a_t[AR];
+  ALoader<AR, AMODE, UNI> al;
+  al.init(p, m0, srow, ROWS_A, c4);
+  // ---- W staging geometry: 16-B chunk (row, part 0..3); loads i < BR/2
+  // fill the hi image, the rest the lo image (image choice wave-uniform)
+  constexpr int BH = BR / 2;
+  static_assert(BR % 2 == 0, "BR must be even");
+  const int bpart = tid & 3;
+  const __amdgpu_buffer_rsrc_t rwhi = make_rsrc(whi);
+  const __amdgpu_buffer_rsrc_t rwlo = make_rsrc(wlo);
+  int boff[BH];
 #pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int m = m0 + srow + ROWS_A * i;
-    a_m[i] = m;
-    a_t[i] = (m < p.M) ? (m % p.T) : -0x40000000;
-  }
-  // ---- W staging geometry: chunk = (row, part); parts 0-3 hi, 4-7 lo
-  const int bpart = tid & 7;
-  const __bf16* bsrc[BR];
-#pragma unroll
-  for (int i = 0; i < BR; ++i) {
-    const int row = (tid + NT * i) >> 3;
-    bsrc[i] = ((bpart < 4) ? whi : wlo) + (size_t)(n0 + row) * p.Kp + (bpart & 3) * 8;
+  for (int i = 0; i < BH; ++i) {
+    const int row = (tid + NT * i) >> 2;
+    boff[i] = ((n0 + row) * p.Kp + bpart * 8) * 2;
   }
 
-  f32x4 ra[AR];
-  bf16x8 rb[BR];
+  // Two register sets: tile k+1 is converted and written to LDS while tile k
+  // is multiplied, and tile k+2 is in flight (loads get a whole k-step of
+  // MFMA time to land before anyone waits on them).
+  f32x4 ra0[AR], ra1[AR];
+  bf16x8 rb0[BR], rb1[BR];
 
-  auto load_tile = [&](int k0) {
-    const int k = k0 + c4;
-    int j = 0, c = 0;
-    const bool kin = k < p.K;
-    if (kin) {
-      j = k / p.cin;
-      c = k - j * p.cin;
-    }
-    const int off = j * p.dil - p.pad;
-    int seg = 0, cl = c;
-    if (AMODE == kACat) {
-      seg = (c >= p.cseg[1]) + (c >= p.cseg[2]);
-      cl = c - p.cseg[seg];
-    }
-    const float* base = (seg == 0) ? p.a[0] : ((seg == 1) ? p.a[1] : p.a[2]);
-    const int ld = (seg == 0) ? p.lda[0] : ((seg == 1) ? p.lda[1] : p.lda[2]);
+  auto load_tile = [&](f32x4 (&ra)[AR], bf16x8 (&rb)[BR], int k0, bool live) {
 #pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int tt = a_t[i] + off;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (kin && tt >= 0 && tt < p.T) {
-        const long row = (long)a_m[i] + off;
-        if (AMODE == kACat) {
-          v = *reinterpret_cast<const f32x4*>(base + row * ld + cl);
-        } else {
-          const f32x4 x0 = *reinterpret_cast<const f32x4*>(p.a[0] + row * p.lda[0] + c);
-          const f32x4 x1 = *reinterpret_cast<const f32x4*>(p.a[1] + row * p.lda[1] + c);
-          v = x0 + x1;
-        }
-      }
-      ra[i] = v;
+    for (int i = 0; i < BH; ++i) {
+      const int o = live ? boff[i] + k0 * 2 : kOOB;
+      rb[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rwhi, o, 0, 0));
+      rb[BH + i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rwlo, o, 0, 0));
     }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) rb[i] = *reinterpret_cast<const bf16x8*>(bsrc[i] + k0);
+    al.load(k0, ra, live);
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](const f32x4 (&ra)[AR], const bf16x8 (&rb)[BR], int buf) {
     unsigned char* st = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
@@ -121,19 +99,19 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float x = ra[i][e];
-        const __bf16 h = (__bf16)x;
-        hi[e] = h;
-        lo[e] = (__bf16)(x - (float)h);
+        const __bf16 hh = (__bf16)x;
+        hi[e] = hh;
+        lo[e] = (__bf16)(x - (float)hh);
       }
       const int off = (srow + ROWS_A * i) * ROWB + c4 * 2;
       *reinterpret_cast<bf16x4*>(st + off) = hi;
       *reinterpret_cast<bf16x4*>(st + A_BYTES + off) = lo;
     }
 #pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int row = (tid + NT * i) >> 3;
-      const int off = 2 * A_BYTES + ((bpart < 4) ? 0 : B_BYTES) + row * ROWB + (bpart & 3) * 16;
+    for (int i = 0; i < BH; ++i) {
+      const int off = 2 * A_BYTES + ((tid + NT * i) >> 2) * ROWB + bpart * 16;
       *reinterpret_cast<bf16x8*>(st + off) = rb[i];
+      *reinterpret_cast<bf16x8*>(st + off + B_LO) = rb[BH + i];
     }
   };
 
@@ -150,42 +128,55 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nk = p.Kp / BK;
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile((kt + 1) * BK);
-    const unsigned char* st = smem + cur * STAGE;
-    const unsigned char* a_hi = st + (wm * TM * 32 + r32) * ROWB + h * 16;
+  auto mma_step = [&](int buf, int s) {
+    const unsigned char* st = smem + buf * STAGE;
+    const unsigned char* a_hi = st + (wm * TM * 32 + r32) * ROWB + h * 16 + s * 32;
     const unsigned char* a_lo = a_hi + A_BYTES;
-    const unsigned char* b_hi = st + 2 * A_BYTES + (wn * TN * 32 + r32) * ROWB + h * 16;
-    const unsigned char* b_lo = b_hi + B_BYTES;
+    const unsigned char* b_hi = st + 2 * A_BYTES + (wn * TN * 32 + r32) * ROWB + h * 16 + s * 32;
+    const unsigned char* b_lo = b_hi + B_LO;
+    bf16x8 ah[TM], al_[TM], bh[TN], bl[TN];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+    for (int i = 0; i < TM; ++i) {
+      ah[i] = *reinterpret_cast<const bf16x8*>(a_hi + i * 32 * ROWB);
+      al_[i] = *reinterpret_cast<const bf16x8*>(a_lo + i * 32 * ROWB);
+    }
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        ah[i] = *reinterpret_cast<const bf16x8*>(a_hi + i * 32 * ROWB + s * 32);
-        al[i] = *reinterpret_cast<const bf16x8*>(a_lo + i * 32 * ROWB + s * 32);
-      }
+    for (int j = 0; j < TN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(b_hi + j * 32 * ROWB);
+      bl[j] = *reinterpret_cast<const bf16x8*>(b_lo + j * 32 * ROWB);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        bh[j] = *reinterpret_cast<const bf16x8*>(b_hi + j * 32 * ROWB + s * 32);
-        bl[j] = *reinterpret_cast<const bf16x8*>(b_lo + j * 32 * ROWB + s * 32);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al_[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-        }
-    }
-    if (kt + 1 < nk) store_tile(cur ^ 1);
+  };
+
+  const int nk = p.Kp / BK;
+  load_tile(ra0, rb0, 0, true);
+  load_tile(ra1, rb1, BK, true);
+  store_tile(ra0, rb0, 0);
+  __syncthreads();
+
+  // nk is even (Kp % 64 == 0, checked on the host).  Loads and stores are
+  // unconditional (past-the-end tiles load zeros into a buffer nobody reads),
+  // so the waitcnt pass sees one straight-line stream: the wait before
+  // store_tile(R) only covers R's loads, issued one k-step earlier.
+  for (int kt = 0; kt < nk; kt += 2) {
+    // even step: compute buffer 0 (tile kt); R1 = tile kt+1 -> buffer 1
+    load_tile(ra0, rb0, (kt + 2) * BK, kt + 2 < nk);
+    mma_step(0, 0);
+    store_tile(ra1, rb1, 1);
+    mma_step(0, 1);
+    __syncthreads();
+    // odd step: compute buffer 1 (tile kt+1); R0 = tile kt+2 -> buffer 0
+    load_tile(ra1, rb1, (kt + 3) * BK, kt + 3 < nk);
+    mma_step(1, 0);
+    store_tile(ra0, rb0, 0);
+    mma_step(1, 1);
     __syncthreads();
   }
 
@@ -216,31 +207,39 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   }
 }
 
-template <int WM, int WN, int TM, int TN>
-void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE>
+void launch_x3_k(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
-  const size_t lds = (size_t)2 * (2 * BM * ROWB + 2 * BN * ROWB);
-  if (p.amode == kAAdd)
-    hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, kAAdd>), dim3(nwg), dim3(NT), lds, s, p, whi, wlo);
-  else
-    hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, kACat>), dim3(nwg), dim3(NT), lds, s, p, whi, wlo);
+  const size_t lds = (size_t)2 * (2 * BM * ROWB + 2 * BN * ROWB + 64);
+  hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, AMODE, UNI, ROLE>), dim3(nwg), dim3(NT), lds, s, p,
+                     whi, wlo);
   WSP_HIP(hipGetLastError());
+}
+
+template <int WM, int WN, int TM, int TN>
+void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
+  const bool uni = uniform_ktiles(p);
+  if (p.amode == kAAdd) {
+    if (uni)
+      launch_x3_k<WM, WN, TM, TN, kAAdd, true, 0>(p, whi, wlo, s);
+    else
+      launch_x3_k<WM, WN, TM, TN, kAAdd, false, 0>(p, whi, wlo, s);
+  } else if (!uni) {
+    launch_x3_k<WM, WN, TM, TN, kACat, false, 0>(p, whi, wlo, s);
+  } else if (p.role == 1) {
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 1>(p, whi, wlo, s);
+  } else {
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 0>(p, whi, wlo, s);
+  }
 }
 
 }  // namespace
 
 void launch_conv_gemm_x3(const ConvGemmArgs& p, const void* whi, const void* wlo, int variant,
                          hipStream_t s) {
-  WSP_CHECK(p.M > 0 && p.N > 0 && p.K > 0 && p.T > 0, "conv_gemm_x3: empty shape");
-  WSP_CHECK(p.cin % 4 == 0, "conv_gemm_x3: cin must be a multiple of 4");
-  WSP_CHECK(p.Kp % BK == 0 && p.Kp >= p.K, "conv_gemm_x3: bad packed K");
-  WSP_CHECK(p.N % 64 == 0, "conv_gemm_x3: N must be a multiple of 64");
-  for (int i = 0; i < 3; ++i) WSP_CHECK(p.lda[i] % 4 == 0, "conv_gemm_x3: lda must be a multiple of 4");
-  if (p.amode == kACat) {
-    WSP_CHECK(p.cseg[0] == 0 && p.cseg[3] == p.cin, "conv_gemm_x3: bad channel segments");
-    for (int i = 1; i < 3; ++i) WSP_CHECK(p.cseg[i] % 4 == 0, "conv_gemm_x3: segment not float4 aligned");
-  }
+  check_conv_args(p, "conv_gemm_x3");
+  WSP_CHECK(p.Kp % 64 == 0, "conv_gemm_x3: packed K must be a multiple of 64");
   const __bf16* h = static_cast<const __bf16*>(whi);
   const __bf16* l = static_cast<const __bf16*>(wlo);
   if (p.N % 128 != 0) {

@@ -38,6 +38,7 @@ struct ConvGemmArgs {
   int ldo;
   int act;
   int amode;
+  int role;  // 1 = SE-Res2Block 1x1 CxC conv (own kernel symbol for profiling)
 };
 
 // bf16x3 split-precision variant (conv_gemm_x3.hip); whi/wlo = packed [N][Kp]

@@ -129,7 +129,7 @@ struct Model::Impl {
 
   // 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA
   int precision = 1;
-  int x3_variant = 0;
+  int x3_variant = 1;
 
   // profiling
   bool prof = false;
@@ -176,7 +176,7 @@ struct Model::Impl {
     cw.cin = cin;
     cw.taps = taps;
     cw.K = cin * taps;
-    cw.Kp = round_up(cw.K, 32);
+    cw.Kp = round_up(cw.K, 64);  // even number of 32-wide k-tiles (bf16x3 pipeline)
     std::vector<float> packed((size_t)N * cw.Kp, 0.f);
     for (int n = 0; n < N; ++n)
       for (int c = 0; c < cin; ++c)
@@ -332,8 +332,9 @@ struct Model::Impl {
 
   void gemm(const char* tag, const ConvW& cw, const float* a0, int lda, float* out, int ldo, int M,
             int T, int dil, int pad, int act, hipStream_t s, const float* row_bias = nullptr,
-            bool use_bias = true) {
+            bool use_bias = true, int role = 0) {
     ConvGemmArgs g{};
+    g.role = role;
     g.a[0] = g.a[1] = g.a[2] = a0;
     g.lda[0] = g.lda[1] = g.lda[2] = lda;
     g.cseg[0] = 0;
@@ -406,7 +407,7 @@ struct Model::Impl {
       const Block& b = blk[li];
       const int dil = li + 2;
       const float* xin = x[li + 1];
-      gemm("conv1x1_CxC", b.c1, xin, C, h1, C, M, T, 1, 0, kActRelu, s);
+      gemm("conv1x1_CxC", b.c1, xin, C, h1, C, M, T, 1, 0, kActRelu, s, nullptr, true, 1);
       for (int i = 0; i < 7; ++i) {
         ConvGemmArgs g{};
         if (i == 0) {
@@ -436,6 +437,7 @@ struct Model::Impl {
         g.cseg[1] = 7 * w;
         g.cseg[2] = g.cseg[3] = C;
         fill(g, b.c3, M, T, 1, 0, h3, C, kActRelu, nullptr, true);
+        g.role = 1;
         run("conv1x1_CxC", 2.0 * M * C * C, s, [&] { launch(g, b.c3, s); });
       }
       run("se", 0, s, [&] {
