@@ -1,0 +1,187 @@
+"""GPU tests of the drop-in API surface (config C1: ECAPA c512 + fbank on a
+10-utterance wav.scp) and of the batch / scoring CLIs, against the CPU oracle.
+Model directory = config.yaml + avg_model.pt (seeded synthetic weights, saved
+with torch.save and loaded back with weights_only=True)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+pytestmark = pytest.mark.gpu
+
+from oracle import fbank_ref, models_ref, scoring_ref  # noqa: E402
+from wespeaker_hubert_amd import arch as A  # noqa: E402
+from wespeaker_hubert_amd.audio import write_wav  # noqa: E402
+from wespeaker_hubert_amd.kaldi_io import load_scp_sequential  # noqa: E402
+from wespeaker_hubert_amd.synthetic import synth_audio, synth_state_dict  # noqa: E402
+
+ARCH = "ECAPA_TDNN_c512"
+
+
+def _cos(a, b):
+    a = a.astype(np.float64)
+    b = b.astype(np.float64)
+    return float(a @ b / np.linalg.norm(a) / np.linalg.norm(b))
+
+
+@pytest.fixture(scope="module")
+def model_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("model")
+    spec = A.make_spec(ARCH, feat_dim=80, embed_dim=192)
+    sd = synth_state_dict(31, A.param_list(spec))
+    ckpt = {k: torch.from_numpy(v) for k, v in sd.items()}
+    ckpt["projection.weight"] = torch.zeros(4, 192)  # training head present in real avg_model.pt
+    torch.save(ckpt, d / "avg_model.pt")
+    cfg = {"model": ARCH, "model_args": {"feat_dim": 80, "embed_dim": 192, "pooling_func": "ASTP"},
+           "dataset_args": {"frontend": "fbank", "resample_rate": 16000, "num_frms": 200,
+                            "fbank_args": {"num_mel_bins": 80, "frame_shift": 10, "frame_length": 25}}}
+    with open(d / "config.yaml", "w") as f:
+        yaml.safe_dump(cfg, f)
+    return str(d), sd
+
+
+@pytest.fixture(scope="module")
+def wav_scp(tmp_path_factory):
+    d = tmp_path_factory.mktemp("wavs")
+    lens = [16000, 24011, 32000, 8801, 48000, 16160, 40400, 12000, 20000, 36123]
+    lines, pcms = [], {}
+    for i, n in enumerate(lens):
+        pcm = synth_audio(500 + i, 1, n)[0]
+        p = str(d / f"u{i:02d}.wav")
+        write_wav(p, pcm)
+        pcms[f"u{i:02d}"] = pcm
+        lines.append(f"u{i:02d} {p}")
+    scp = str(d / "wav.scp")
+    with open(scp, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    raw = str(d / "raw.list")
+    with open(raw, "w") as f:
+        for ln in lines:
+            k, p = ln.split()
+            f.write(json.dumps({"key": k, "wav": p, "spk": "s" + k[-1]}) + "\n")
+    return scp, raw, pcms
+
+
+def _oracle_embed(sd, pcm):
+    feats = fbank_ref.fbank(pcm, cmn=True)[None]
+    with torch.no_grad():
+        _, e = models_ref.forward(ARCH, torch.from_numpy(feats), {k: torch.from_numpy(v) for k, v in sd.items()})
+    return e[0].numpy()
+
+
+def test_load_model_extract_embedding_list(model_dir, wav_scp):
+    import wespeaker_hubert_amd as wespeaker
+    d, sd = model_dir
+    scp, _, pcms = wav_scp
+    spk = wespeaker.load_model(d)
+    names, embs = spk.extract_embedding_list(scp)
+    assert names == sorted(pcms)
+    for n, e in zip(names, embs):
+        assert e.shape == (192,) and e.dtype == np.float32
+        ref = _oracle_embed(sd, pcms[n])
+        assert _cos(e, ref) >= 0.9999
+        assert np.abs(e - ref).max() < 2e-3  # fbank fp32 rounding propagates (see test_gpu_parity)
+    sim = spk.compute_similarity(scp.replace("wav.scp", "u00.wav"), scp.replace("wav.scp", "u01.wav"))
+    e0 = _oracle_embed(sd, pcms["u00"])
+    e1 = _oracle_embed(sd, pcms["u01"])
+    assert abs(sim - (_cos(e0, e1) + 1) / 2) < 1e-4
+
+
+def test_cli_embedding_kaldi(model_dir, wav_scp, tmp_path):
+    from wespeaker_hubert_amd.cli.speaker import main
+    d, sd = model_dir
+    scp, _, pcms = wav_scp
+    out = str(tmp_path / "emb")
+    main(["--task", "embedding_kaldi", "-p", d, "--wav_scp", scp, "--output_file", out])
+    got = dict(load_scp_sequential(out + ".scp"))
+    assert sorted(got) == sorted(pcms)
+    for k, e in got.items():
+        assert _cos(e, _oracle_embed(sd, pcms[k])) >= 0.9999
+
+
+@pytest.mark.parametrize("batch_size", [1, 4])
+def test_extract_driver_raw_list(model_dir, wav_scp, tmp_path, batch_size):
+    from wespeaker_hubert_amd.bin.extract import extract
+    d, sd = model_dir
+    _, raw, pcms = wav_scp
+    ark = str(tmp_path / "xvector.ark")
+    scp = extract(config=os.path.join(d, "config.yaml"), model_path=os.path.join(d, "avg_model.pt"),
+                  data_type="raw", data_list=raw, embed_ark=ark, batch_size=batch_size, num_workers=2)
+    got = dict(load_scp_sequential(scp))
+    assert sorted(got) == sorted(pcms)
+    if batch_size == 1:
+        for k, e in got.items():
+            assert _cos(e, _oracle_embed(sd, pcms[k])) >= 0.9999
+    else:  # random 2.0 s chunks: deterministic for a fixed chunk_seed
+        scp2 = extract(config=os.path.join(d, "config.yaml"), model_path=os.path.join(d, "avg_model.pt"),
+                       data_type="raw", data_list=raw, embed_ark=str(tmp_path / "x2.ark"), batch_size=batch_size)
+        got2 = dict(load_scp_sequential(scp2))
+        for k in got:
+            np.testing.assert_allclose(got[k], got2[k], atol=1e-6)
+
+
+def test_scoring_pipeline_matches_oracle(tmp_path):
+    """score.py -> vector_mean.py -> score_norm.py -> compute_metrics.py on synthetic embeddings."""
+    from wespeaker_hubert_amd.bin import score, score_norm, vector_mean
+    from wespeaker_hubert_amd.kaldi_io import WriteHelper
+    from wespeaker_hubert_amd.scoring import compute_metrics
+    rng = np.random.default_rng(3)
+    D, n_spk, per = 64, 40, 5
+    centers = rng.standard_normal((n_spk, D))
+    eval_dir = tmp_path / "vox1"
+    dev_dir = tmp_path / "dev"
+    eval_dir.mkdir()
+    dev_dir.mkdir()
+    evals, devs = {}, {}
+    for s in range(n_spk):
+        for u in range(per):
+            evals[f"e{s:02d}-{u}"] = (centers[s] + 0.8 * rng.standard_normal(D)).astype(np.float32)
+            devs[f"d{s:02d}-{u}"] = (rng.standard_normal(D) + 0.3).astype(np.float32)
+    for path, emb in ((eval_dir, evals), (dev_dir, devs)):
+        with WriteHelper(f"ark,scp:{path}/xvector.ark,{path}/xvector.scp") as w:
+            for k, v in emb.items():
+                w(k, v)
+    keys = list(evals)
+    trial = tmp_path / "trials"
+    with open(trial, "w") as f:
+        for i in range(600):
+            a, b = rng.choice(len(keys), 2, replace=False)
+            lab = "target" if keys[a][:3] == keys[b][:3] else "nontarget"
+            f.write(f"{keys[a]} {keys[b]} {lab}\n")
+    score.main(str(tmp_path), str(eval_dir / "xvector.scp"), True, str(dev_dir), str(trial))
+    mean_vec = np.stack(list(devs.values())).astype(np.float64).mean(0)
+    np.testing.assert_allclose(np.load(dev_dir / "mean_vec.npy"), mean_vec, atol=1e-6)
+    lines = open(tmp_path / "scores" / "trials.score").read().splitlines()
+    for ln in lines[:50]:
+        a, b, s, lab = ln.split()
+        ref = scoring_ref.cosine(evals[a] - mean_vec.astype(np.float32), evals[b] - mean_vec.astype(np.float32))
+        assert abs(float(s) - ref) <= 6e-6  # printed with {:.5f}
+    # cohort = per-speaker means of dev
+    with open(tmp_path / "spk2utt", "w") as f:
+        for s in range(n_spk):
+            f.write(f"S{s:02d} " + " ".join(f"d{s:02d}-{u}" for u in range(per)) + "\n")
+    vector_mean.compute_vector_mean(str(tmp_path / "spk2utt"), str(dev_dir / "xvector.scp"),
+                                    str(dev_dir / "spk_xvector.ark"))
+    cohort = dict(load_scp_sequential(str(dev_dir / "spk_xvector.scp")))
+    np.testing.assert_allclose(cohort["S03"], np.stack([devs[f"d03-{u}"] for u in range(per)]).mean(0), atol=1e-6)
+    out = tmp_path / "scores" / "asnorm.score"
+    score_norm.main("asnorm", 10, str(tmp_path / "scores" / "trials.score"), str(out),
+                    str(dev_dir / "spk_xvector.scp"), str(eval_dir / "xvector.scp"),
+                    str(dev_dir / "mean_vec.npy"))
+    mv = np.load(dev_dir / "mean_vec.npy")
+    C = np.stack(list(cohort.values()))
+    for ln in open(out).read().splitlines()[:30]:
+        e, t, ns = ln.split()[:3]
+        s = float([x for x in lines if x.startswith(f"{e} {t} ")][0].split()[2])
+        emu, esd = scoring_ref.get_mean_std((evals[e] - mv)[None], C - mv, 10)
+        tmu, tsd = scoring_ref.get_mean_std((evals[t] - mv)[None], C - mv, 10)
+        ref = scoring_ref.asnorm(s, emu[0], esd[0], tmu[0], tsd[0])
+        assert abs(float(ns) - ref) <= 2e-5
+    eer, mindcf = compute_metrics(str(tmp_path / "scores" / "trials.score"))
+    sc = np.array([float(x.split()[2]) for x in lines])
+    lab = np.array([x.split()[3] == "target" for x in lines])
+    fnr, fpr = scoring_ref.compute_pmiss_pfa_rbst(sc, lab)
+    assert abs(eer - 100 * scoring_ref.compute_eer(fnr, fpr)) < 1e-9

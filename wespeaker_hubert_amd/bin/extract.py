@@ -1,0 +1,195 @@
+"""Batch embedding extraction driver — drop-in for wespeaker/bin/extract.py.
+
+Same flags as the reference (fire-style; `tools/extract_embedding.sh:51-62`):
+  --config --model_path --data_type {raw,shard} --data_list --embed_ark
+  --batch-size --num-workers [--reverb_data --noise_data --aug-prob]
+Writes `<embed_ark>` and `<embed_ark[:-3]>scp` (extract.py:86-88).
+
+Semantics (bin/extract.py:33-120, dataset/dataset.py:136-247):
+  * batch_size == 1: whole utterances; batch_size > 1: one random chunk of
+    ((num_frms-1)*frame_shift + frame_length)*sr/1000 samples per utterance
+    (processor.get_random_chunk, repeat-padded when shorter) — seeded here
+    (`--chunk_seed`, default 0) so extraction is reproducible;
+  * fbank on the GPU with dither 0, CMN (apply_cmvn norm_mean) fused;
+  * under torchrun (WORLD_SIZE > 1) the data list is split into contiguous
+    parts exactly like tools/extract_embedding.sh:40-42 and rank r writes
+    `<embed_ark stem>_<r:03d>.ark/.scp` (cat the scps in rank order).
+Audio decode runs on a host thread pool (`--num-workers`); augmentation
+(aug_prob > 0) and the s3prl front end are not available on this path.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import logging
+import os
+import random
+import sys
+import tarfile
+import io
+from concurrent.futures import ThreadPoolExecutor
+from typing import Iterator, List, Tuple
+
+import numpy as np
+import torch
+import yaml
+
+from .. import audio
+from ..frontend import compute_fbank
+from ..kaldi_io import WriteHelper, validate_path
+from ..speaker_model import get_speaker_model
+from . import _fire
+
+AUDIO_EXT = {"wav"}
+
+
+def parse_config_or_kwargs(config_file, **kwargs):
+    """utils/utils.py:37-51."""
+    with open(config_file) as f:
+        cfg = yaml.safe_load(f)
+    return dict(cfg, **kwargs)
+
+
+def read_lists(path: str) -> List[str]:
+    with open(path, "r", encoding="utf8") as f:
+        return [ln.strip() for ln in f if ln.strip()]
+
+
+def iter_raw(lines: List[str]) -> Iterator[Tuple[str, str, list]]:
+    for ln in lines:
+        obj = json.loads(ln)
+        yield obj["key"], obj["wav"], obj.get("vad")
+
+
+def decode_raw(item) -> Tuple[str, np.ndarray, int]:
+    key, wav, vad = item
+    pcm, sr = audio.load_wav(wav)
+    x = pcm[0]
+    if vad:  # processor.parse_raw apply_vad: concatenate voiced segments
+        x = np.concatenate([x[int(float(s) * sr):int(float(e) * sr)] for s, e in vad])
+    return key, x, sr
+
+
+def iter_shard(lines: List[str]) -> Iterator[Tuple[str, np.ndarray, int]]:
+    """processor.tar_file_and_group: files grouped by prefix, audio by extension."""
+    for path in lines:
+        with tarfile.open(path, mode="r:*") as tar:
+            for ti in tar:
+                prefix, _, ext = ti.name.rpartition(".")
+                if ext in AUDIO_EXT:
+                    data = tar.extractfile(ti).read()
+                    tmp = io.BytesIO(data)
+                    import wave
+                    with wave.open(tmp, "rb") as w:
+                        sr = w.getframerate()
+                        ch = w.getnchannels()
+                        raw = w.readframes(w.getnframes())
+                    x = np.frombuffer(raw, dtype="<i2").reshape(-1, ch)[:, 0].copy()
+                    yield prefix, x, sr
+
+
+def get_random_chunk(data: np.ndarray, chunk_len: int, rng: random.Random) -> np.ndarray:
+    """processor.py:291-323."""
+    n = len(data)
+    if n >= chunk_len:
+        s = rng.randint(0, n - chunk_len)
+        return data[s:s + chunk_len].copy()
+    reps = chunk_len // n + 1
+    return np.tile(data, reps)[:chunk_len]
+
+
+def extract(config="conf/config.yaml", **kwargs):
+    configs = parse_config_or_kwargs(config, **kwargs)
+    model_path = configs["model_path"]
+    embed_ark = configs["embed_ark"]
+    batch_size = int(configs.get("batch_size", 1))
+    num_workers = max(1, int(configs.get("num_workers", 1)))
+    test_conf = copy.deepcopy(configs["dataset_args"])
+    frontend_type = test_conf.get("frontend", "fbank")
+    if frontend_type != "fbank":
+        raise NotImplementedError(f"frontend {frontend_type!r} is not available on the MI355X path yet")
+    if float(configs.get("aug_prob", 0.0) or 0.0) > 0:
+        logging.warning("aug_prob > 0 ignored: augmentation is out of scope at extraction")
+    cmvn_args = test_conf.get("cmvn_args", {}) or {}
+    if cmvn_args.get("norm_var", False) or not cmvn_args.get("norm_mean", True):
+        raise NotImplementedError("only apply_cmvn(norm_mean=True, norm_var=False) is implemented")
+    if not test_conf.get("cmvn", True):
+        raise NotImplementedError("cmvn=False is not implemented")
+    fb = test_conf.get("fbank_args", {})
+    if int(fb.get("num_mel_bins", 80)) != 80 or int(fb.get("frame_shift", 10)) != 10 \
+            or int(fb.get("frame_length", 25)) != 25:
+        raise NotImplementedError("fbank implemented for 80 bins, 25/10 ms")
+    sr_target = int(test_conf.get("resample_rate", 16000))
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.device_count() > 1:
+        torch.cuda.set_device(local % torch.cuda.device_count())
+    device = torch.device("cuda", torch.cuda.current_device())
+
+    model = get_speaker_model(configs["model"])(**configs["model_args"])
+    state = torch.load(model_path, map_location="cpu", weights_only=True)
+    model.load_state_dict(state, strict=False)
+    model.to(device)
+
+    lines = read_lists(configs["data_list"])
+    if world > 1:  # tools/extract_embedding.sh:40-42 contiguous split
+        per = len(lines) // world + 1
+        lines = lines[rank * per:(rank + 1) * per]
+        stem = embed_ark[:-4] if embed_ark.endswith(".ark") else embed_ark
+        embed_ark = f"{stem}_{rank:03d}.ark"
+    validate_path(embed_ark)
+    embed_ark = os.path.abspath(embed_ark)
+    embed_scp = embed_ark[:-3] + "scp"
+
+    data_type = configs["data_type"]
+    if data_type == "raw":
+        pool = ThreadPoolExecutor(num_workers)
+        stream = pool.map(decode_raw, iter_raw(lines))
+    elif data_type == "shard":
+        stream = iter_shard(lines)
+    else:
+        raise NotImplementedError(f"data_type {data_type!r}")
+
+    rng = random.Random(int(configs.get("chunk_seed", 0)))
+    num_frms = int(test_conf.get("num_frms", 200))
+    chunk_len = ((num_frms - 1) * 10 + 25) * sr_target // 1000
+
+    def run(keys, wavs, writer):
+        x = torch.from_numpy(np.stack(wavs).astype(np.float32)).to(device)
+        feats = compute_fbank(x, scale=1.0, cmn=True)
+        emb = model(feats)[-1].cpu().numpy()
+        for k, e in zip(keys, emb):
+            writer(k, e)
+
+    n = 0
+    with torch.no_grad(), WriteHelper("ark,scp:" + embed_ark + "," + embed_scp) as writer:
+        keys, wavs = [], []
+        for key, x, sr in stream:
+            if sr != sr_target:
+                raise NotImplementedError(f"{key}: sample rate {sr} != {sr_target} (resampling not implemented)")
+            if batch_size == 1:
+                run([key], [x], writer)
+            else:
+                keys.append(key)
+                wavs.append(get_random_chunk(x, chunk_len, rng))
+                if len(keys) == batch_size:
+                    run(keys, wavs, writer)
+                    keys, wavs = [], []
+            n += 1
+        if keys:
+            run(keys, wavs, writer)
+    print(f"extracted {n} embeddings -> {embed_scp}")
+    return embed_scp
+
+
+def main(argv=None):
+    pos, kw = _fire.parse(sys.argv[1:] if argv is None else argv)
+    if pos:
+        kw.setdefault("config", pos[0])
+    extract(**kw)
+
+
+if __name__ == "__main__":
+    main()
