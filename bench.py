@@ -28,7 +28,25 @@ from wespeaker_hubert_amd.speaker_model import HipSpeakerModel  # noqa: E402
 from wespeaker_hubert_amd.synthetic import synth_audio, synth_state_dict  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (no sparsity)
 HBM_PEAK_GBPS = 8000.0
+DOMINANT = {  # kernel symbol of the SE-Res2Block 1x1 CxC conv (ConvGemmArgs.role == 1)
+    1: "_ZN3wsp12_GLOBAL__N_112conv_gemm_x3ILi4ELi2ELi2ELi2ELi0ELb1ELi1EEEvNS_12ConvGemmArgsEPKDF16bS4_",
+    0: "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1EEEvNS_12ConvGemmArgsE",
+}
+
+
+def profiled_traffic(symbol: str, grid: int):
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary
+    (profiles/*_traffic.json, made by scripts/make_profile_summary.py)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        d = json.load(open(f))
+        v = d.get(f"{symbol}|{grid}")
+        if v:
+            return v["hbm_bytes"], os.path.basename(f)
+    return None, None
 
 
 def parse():
@@ -148,12 +166,22 @@ def main():
         k = kernels.get("conv1x1_CxC")
         if k:
             C = 1024 if "c1024" in args.arch else 512
-            flops = 2.0 * B * T * C * C          # algorithmic: 2*M*N*K, M = B*T frames
+            M = B * T
+            flops = 2.0 * M * C * C          # algorithmic: 2*M*N*K, M = B*T frames
             ach = flops / (k["avg_ms"] * 1e-3) / 1e12
-            roof = {"kernel": "conv_gemm_f32<2,2,2,2,kACat> (SE-Res2Block 1x1 conv CxC)",
-                    "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                    "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"]}
+            x3 = args.precision == 1
+            peak = BF16_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+            sym = DOMINANT[args.precision]
+            grid = (M // 256) * (C // 128) * 512 if x3 else ((M + 127) // 128) * (C // 128) * 256
+            traffic, src = profiled_traffic(sym, grid)
+            algo_bytes = 4.0 * M * C * 2 + (2 if x3 else 4) * C * C * (2 if x3 else 1)
+            roof = {"kernel": sym, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                    "traffic": traffic, "traffic_source": src, "algorithmic_bytes": algo_bytes,
+                    "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"],
+                    "mfma_dtype": "bf16 (3-term split, fp32 accumulate)" if x3 else "f32",
+                    "mfma_work_factor": 3 if x3 else 1,
+                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4)}
 
     gf = ecapa_gflop_per_utt(spec, T)
     res = {

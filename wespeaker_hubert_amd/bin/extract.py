@@ -35,6 +35,7 @@ import torch
 import yaml
 
 from .. import audio
+from ..dist import shard_lines
 from ..frontend import compute_fbank
 from ..kaldi_io import WriteHelper, validate_path
 from ..speaker_model import get_speaker_model
@@ -135,8 +136,7 @@ def extract(config="conf/config.yaml", **kwargs):
 
     lines = read_lists(configs["data_list"])
     if world > 1:  # tools/extract_embedding.sh:40-42 contiguous split
-        per = len(lines) // world + 1
-        lines = lines[rank * per:(rank + 1) * per]
+        lines = shard_lines(lines, rank, world)
         stem = embed_ark[:-4] if embed_ark.endswith(".ark") else embed_ark
         embed_ark = f"{stem}_{rank:03d}.ark"
     validate_path(embed_ark)
