@@ -107,9 +107,10 @@ def main():
 
     B = args.batch
     N = int(round(args.seconds * 16000))
-    spec = make_spec(args.arch, feat_dim=80, embed_dim=192)
-    model = HipSpeakerModel(args.arch, feat_dim=80, embed_dim=192)
-    sd = synth_state_dict(1234, model.state_dict_layout())
+    emb_dim = 192 if args.arch.startswith("ECAPA") else 256
+    spec = make_spec(args.arch, feat_dim=80, embed_dim=emb_dim)
+    model = HipSpeakerModel(args.arch, feat_dim=80, embed_dim=emb_dim)
+    sd = synth_state_dict(1234, model.state_dict_layout(), residual_tame=args.arch.startswith("ResNet"))
     model.load_state_dict(sd)
     model.set_option("precision", args.precision)
     if args.x3_variant is not None:
@@ -120,7 +121,7 @@ def main():
     wav = torch.from_numpy(synth_audio(7 + rank, B, N)).to(dev)
     T = 1 + (N - 400) // 160
     feats = torch.empty(B, T, 80, device=dev)
-    emb = torch.empty(B, 192, device=dev)
+    emb = torch.empty(B, emb_dim, device=dev)
 
     def step():
         compute_fbank(wav, scale=1.0, cmn=True, out=feats)
@@ -156,7 +157,7 @@ def main():
     kernels, roof = {}, None
     if not args.no_profile:
         for tag in ("layer1", "conv1x1_CxC", "res2_k3", "se", "conv_cat", "glob_ctx", "pool_linear1",
-                    "pool_linear2", "astp", "head"):
+                    "pool_linear2", "astp", "head", "stem", "shortcut", "res_conv1x1", "res_conv3x3", "tstp_head"):
             n, ms, fl = model.profile_query(tag)
             if n:
                 avg = ms / n
@@ -183,7 +184,8 @@ def main():
                     "mfma_work_factor": 3 if x3 else 1,
                     "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4)}
 
-    gf = ecapa_gflop_per_utt(spec, T)
+    gf = ecapa_gflop_per_utt(spec, T) if args.arch.startswith("ECAPA") else sum(
+        v["ms_per_step"] * (v["tflops"] or 0) for v in kernels.values()) / B if kernels else 0.0
     res = {
         "metric": "embeddings/sec on 5s 16kHz utts",
         "value": round(value, 2),

@@ -10,10 +10,15 @@ run() {
   echo "== $name rc=$rc"; tail -n ${TAILN:-6} "gpurun_out/$name.log"
   return $rc
 }
-run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider; rc=$?
+rc=0
+if [ -z "${SKIP_TESTS:-}" ]; then
+  run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider; rc=$?
+fi
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-for cfg in "--precision 0" "--precision 1 --x3-variant 0" "--precision 1 --x3-variant 1"; do
+# CFGS: bench configurations separated by '|'
+IFS='|' read -ra CFG_LIST <<< "${CFGS:---precision 1 --x3-variant 1}"
+for cfg in "${CFG_LIST[@]}"; do
   tag=$(echo $cfg | tr -d ' -')
-  run bench_$tag 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline $cfg || exit $?
+  run bench_$tag 400 python bench.py --steps 10 --warmup 2 --no-cpu-baseline $cfg || exit $?
 done
 exit $rc

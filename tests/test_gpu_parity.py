@@ -20,6 +20,7 @@ from wespeaker_hubert_amd.synthetic import synth_audio, synth_feats, synth_state
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 ECAPA_FIX = sorted(p for p in glob.glob(os.path.join(GOLD, "ecapa*.npz")))
+RESNET_FIX = sorted(p for p in glob.glob(os.path.join(GOLD, "resnet*.npz")))
 EMB_ATOL = 1e-4
 EMB_COS = 0.9999
 
@@ -50,8 +51,8 @@ def _hip_model(arch, seed, precision=1, variant=1, **kw):
     return m.to(DEV), sd
 
 
-PREC = [(1, 1), (1, 0), (0, 0)]
-PREC_IDS = ["bf16x3_256", "bf16x3_128", "f32"]
+PREC = [(1, 2), (1, 1), (1, 0), (0, 0)]
+PREC_IDS = ["bf16x3_dma", "bf16x3_256", "bf16x3_128", "f32"]
 
 
 @pytest.mark.parametrize("prec", PREC, ids=PREC_IDS)
@@ -78,6 +79,32 @@ def test_ecapa_matches_oracle_batched(arch, B, T, prec):
     # batch independence: each utterance alone gives the same embedding
     _, e0 = m(torch.from_numpy(x[:1]).to(DEV))
     assert np.abs(e0.cpu().numpy() - emb[:1].cpu().numpy()).max() < 1e-5
+
+
+@pytest.mark.parametrize("path", RESNET_FIX, ids=[os.path.basename(p)[:-4] for p in RESNET_FIX])
+def test_resnet_matches_reference_fixture(path):
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    z = np.load(path, allow_pickle=False)
+    m = HipSpeakerModel(str(z["arch"]), feat_dim=int(z["feat_dim"]), embed_dim=int(z["embed_dim"]))
+    m.load_state_dict(synth_state_dict(int(z["weight_seed"]), m.state_dict_layout(), residual_tame=True))
+    m.to(DEV)
+    x = synth_feats(int(z["input_seed"]), int(z["B"]), int(z["T"]), int(z["feat_dim"]))
+    _, emb = m(torch.from_numpy(x).to(DEV))
+    _assert_emb(emb.cpu().numpy(), z["embed"])
+
+
+@pytest.mark.parametrize("arch,B,T", [("ResNet34", 3, 77), ("ResNet50", 2, 131), ("ResNet18", 2, 9)])
+def test_resnet_matches_oracle(arch, B, T):
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    m = HipSpeakerModel(arch, feat_dim=80, embed_dim=256)
+    sd = synth_state_dict(9, m.state_dict_layout(), residual_tame=True)
+    m.load_state_dict(sd)
+    m.to(DEV)
+    x = synth_feats(98, B, T, 80)
+    _, emb = m(torch.from_numpy(x).to(DEV))
+    with torch.no_grad():
+        _, ref = models_ref.forward(arch, torch.from_numpy(x), {k: torch.from_numpy(v) for k, v in sd.items()})
+    _assert_emb(emb.cpu().numpy(), ref.numpy())
 
 
 def test_ecapa_deterministic():

@@ -120,32 +120,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(const ConvGemmArgs p) {
     __syncthreads();
   }
 
-  // ---- epilogue: lane owns column (lane & 31) of each 32x32 tile and rows
-  // (r&3) + 8(r>>2) + 4h, r = 0..15 (gfx950 32x32 C/D map).
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + (wn * TN + j) * 32 + r32;
-    const float bv = p.bias ? p.bias[col] : 0.f;
-    const float sc = p.scale ? p.scale[col] : 1.f;
-    const float sh = p.scale ? p.shift[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rbase = m0 + (wm * TM + i) * 32 + 4 * h;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rbase + (r & 3) + 8 * (r >> 2);
-        if (row < p.M) {
-          float y = acc[i][j][r] + bv;
-          if (p.row_bias) y += p.row_bias[(size_t)(row / p.T) * p.N + col];
-          if (p.res) y += p.res[(size_t)row * p.ldres + col];
-          if (p.act == kActRelu) y = fmaxf(y, 0.f);
-          else if (p.act == kActTanh) y = tanhf(y);
-          if (p.scale) y = y * sc + sh;
-          p.out[(size_t)row * p.ldo + col] = y;
-        }
-      }
-    }
-  }
+  gemm_epilogue<TM, TN>(p, acc, m0, n0, wm, wn, lane);
 }
 
 template <int WM, int WN, int TM, int TN, int AMODE, bool UNI>
@@ -175,6 +150,7 @@ int conv_gemm_tile_for(int N) { return (N % 128 == 0) ? 0 : 1; }
 
 void launch_conv_gemm(const ConvGemmArgs& p, hipStream_t s) {
   check_conv_args(p, "conv_gemm");
+  WSP_CHECK(!p.conv2d && p.N % 64 == 0, "conv_gemm (f32): 1-D convs with N % 64 == 0 only");
   if (conv_gemm_tile_for(p.N) == 0)
     launch_tile<2, 2, 2, 2>(p, s);
   else

@@ -15,6 +15,8 @@
 // hi/lo bf16 while staging; W is pre-split on the host.  LDS rows are
 // 32 bf16 + 8 pad (80 B): the 16-byte fragment reads (row = lane&31,
 // k = 16 s + 8 (lane>>5)) hit 16 distinct slots per ds_read_b128 group.
+#include <type_traits>
+
 #include "gemm_common.h"
 
 namespace wsp {
@@ -27,7 +29,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int BK = 32;
 constexpr int ROWB = 80;  // bytes per LDS row (32 bf16 + 8 pad)
 
-template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE>
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D = false>
 __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArgs p,
                                                                const __bf16* __restrict__ whi,
                                                                const __bf16* __restrict__ wlo) {
@@ -35,13 +37,14 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
   constexpr int AR = BM * 8 / NT;       // float4 A loads per thread per k-tile
-  constexpr int BR = BN * 8 / NT;       // 16-byte W loads per thread per k-tile
+  constexpr int BR = BN * 8 / NT;       // 16-byte W loads per thread per k-tile (hi + lo)
   constexpr int ROWS_A = NT / 8;        // A rows covered per pass
   constexpr int A_BYTES = BM * ROWB;    // one bf16 image (hi or lo) of the A tile
   constexpr int B_BYTES = BN * ROWB;
   constexpr int B_LO = B_BYTES + 64;  // lo image skewed by 16 banks vs hi (conflict-free stores)
   constexpr int STAGE = 2 * A_BYTES + B_LO + B_BYTES;
   static_assert(AR >= 1 && BR >= 1, "tile too small for the thread count");
+  static_assert(BN * 4 % 64 == 0, "a W image must be a whole number of wave loads");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -59,20 +62,23 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   // ---- A staging geometry
   const int srow = tid >> 3;
   const int c4 = (tid & 7) * 4;
-  ALoader<AR, AMODE, UNI> al;
+  std::conditional_t<C2D, ALoader2D<AR>, ALoader<AR, AMODE, UNI>> al;
   al.init(p, m0, srow, ROWS_A, c4);
-  // ---- W staging geometry: 16-B chunk (row, part 0..3); loads i < BR/2
-  // fill the hi image, the rest the lo image (image choice wave-uniform)
-  constexpr int BH = BR / 2;
-  static_assert(BR % 2 == 0, "BR must be even");
-  const int bpart = tid & 3;
+  // ---- W staging geometry: 16-B chunk id q = tid + NT*i over both images
+  // (BN*4 chunks each; image = q / (BN*4) is wave-uniform), row = (q % (BN*4)) >> 2
   const __amdgpu_buffer_rsrc_t rwhi = make_rsrc(whi);
   const __amdgpu_buffer_rsrc_t rwlo = make_rsrc(wlo);
-  int boff[BH];
+  int boff[BR], bls[BR];
+  bool bimg[BR];
 #pragma unroll
-  for (int i = 0; i < BH; ++i) {
-    const int row = (tid + NT * i) >> 2;
-    boff[i] = ((n0 + row) * p.Kp + bpart * 8) * 2;
+  for (int i = 0; i < BR; ++i) {
+    const int q = tid + NT * i;
+    const int img = __builtin_amdgcn_readfirstlane(q / (BN * 4));  // wave-uniform (BN*4 % 64 == 0)
+    const int qq = q - img * BN * 4;
+    const int row = qq >> 2, part = qq & 3;
+    bimg[i] = img != 0;
+    boff[i] = ((n0 + row) * p.Kp + part * 8) * 2;
+    bls[i] = row * ROWB + part * 16 + (img ? B_LO : 0);
   }
 
   // Two register sets: tile k+1 is converted and written to LDS while tile k
@@ -83,10 +89,9 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
 
   auto load_tile = [&](f32x4 (&ra)[AR], bf16x8 (&rb)[BR], int k0, bool live) {
 #pragma unroll
-    for (int i = 0; i < BH; ++i) {
+    for (int i = 0; i < BR; ++i) {
       const int o = live ? boff[i] + k0 * 2 : kOOB;
-      rb[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rwhi, o, 0, 0));
-      rb[BH + i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rwlo, o, 0, 0));
+      rb[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(bimg[i] ? rwlo : rwhi, o, 0, 0));
     }
     al.load(k0, ra, live);
   };
@@ -108,11 +113,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
       *reinterpret_cast<bf16x4*>(st + A_BYTES + off) = lo;
     }
 #pragma unroll
-    for (int i = 0; i < BH; ++i) {
-      const int off = 2 * A_BYTES + ((tid + NT * i) >> 2) * ROWB + bpart * 16;
-      *reinterpret_cast<bf16x8*>(st + off) = rb[i];
-      *reinterpret_cast<bf16x8*>(st + off + B_LO) = rb[BH + i];
-    }
+    for (int i = 0; i < BR; ++i) *reinterpret_cast<bf16x8*>(st + 2 * A_BYTES + bls[i]) = rb[i];
   };
 
   const int wm = wave / WN;
@@ -180,45 +181,25 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
     __syncthreads();
   }
 
-  // ---- epilogue (gfx950 32x32 C/D map: col = lane&31, row = (r&3)+8(r>>2)+4h)
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + (wn * TN + j) * 32 + r32;
-    const float bv = p.bias ? p.bias[col] : 0.f;
-    const float sc = p.scale ? p.scale[col] : 1.f;
-    const float sh = p.scale ? p.shift[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rbase = m0 + (wm * TM + i) * 32 + 4 * h;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rbase + (r & 3) + 8 * (r >> 2);
-        if (row < p.M) {
-          float y = acc[i][j][r] + bv;
-          if (p.row_bias) y += p.row_bias[(size_t)(row / p.T) * p.N + col];
-          if (p.res) y += p.res[(size_t)row * p.ldres + col];
-          if (p.act == kActRelu) y = fmaxf(y, 0.f);
-          else if (p.act == kActTanh) y = tanhf(y);
-          if (p.scale) y = y * sc + sh;
-          p.out[(size_t)row * p.ldo + col] = y;
-        }
-      }
-    }
-  }
+  gemm_epilogue<TM, TN>(p, acc, m0, n0, wm, wn, lane);
 }
 
-template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE>
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D = false>
 void launch_x3_k(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const size_t lds = (size_t)2 * (2 * BM * ROWB + 2 * BN * ROWB + 64);
-  hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, AMODE, UNI, ROLE>), dim3(nwg), dim3(NT), lds, s, p,
-                     whi, wlo);
+  hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, AMODE, UNI, ROLE, C2D>), dim3(nwg), dim3(NT), lds, s,
+                     p, whi, wlo);
   WSP_HIP(hipGetLastError());
 }
 
 template <int WM, int WN, int TM, int TN>
 void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
+  if (p.conv2d) {
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, true>(p, whi, wlo, s);
+    return;
+  }
   const bool uni = uniform_ktiles(p);
   if (p.amode == kAAdd) {
     if (uni)
@@ -242,7 +223,9 @@ void launch_conv_gemm_x3(const ConvGemmArgs& p, const void* whi, const void* wlo
   WSP_CHECK(p.Kp % 64 == 0, "conv_gemm_x3: packed K must be a multiple of 64");
   const __bf16* h = static_cast<const __bf16*>(whi);
   const __bf16* l = static_cast<const __bf16*>(wlo);
-  if (p.N % 128 != 0) {
+  if (p.N % 64 != 0) {
+    launch_x3_tile<4, 1, 1, 1>(p, h, l, s);  // 128 x 32, 4 waves
+  } else if (p.N % 128 != 0) {
     launch_x3_tile<4, 1, 1, 2>(p, h, l, s);  // 128 x 64, 4 waves
   } else if (variant == 1) {
     launch_x3_tile<4, 2, 2, 2>(p, h, l, s);  // 256 x 128, 8 waves

@@ -122,6 +122,114 @@ struct ALoader {
   }
 };
 
+// 2-D NHWC variant (ResNet): rows are output positions (b, fo, to); one
+// segment, cin % 32 == 0 (uniform k-tiles).
+template <int AR>
+struct ALoader2D {
+  const float* a0;
+  int ld, cin, Fi, Ti, kw, T0;
+  int c4;
+  int rb[AR], fi0[AR], ti0[AR];
+  int j, c;
+
+  __device__ __forceinline__ void init(const ConvGemmArgs& p, int m0, int srow, int rows_step,
+                                       int c4_) {
+    a0 = p.a[0];
+    ld = p.lda[0];
+    cin = p.cin;
+    Fi = p.Fi;
+    Ti = p.Ti;
+    kw = p.kw;
+    c4 = c4_;
+    j = 0;
+    c = 0;
+    const int plane = p.Fo * p.To;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = m0 + srow + rows_step * i;
+      const int b = m / plane;
+      const int rem = m - b * plane;
+      const int fo = rem / p.To;
+      const int to = rem - fo * p.To;
+      rb[i] = b * p.Fi * p.Ti;
+      fi0[i] = (m < p.M) ? fo * p.stride - p.pad : -0x40000000;
+      ti0[i] = to * p.stride - p.pad;
+    }
+  }
+
+  __device__ __forceinline__ void load(int /*k0*/, f32x4 (&ra)[AR], bool live = true) {
+    const int kf = j / kw;
+    const int kt = j - kf * kw;
+    const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a0);
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int fi = fi0[i] + kf;
+      const int ti = ti0[i] + kt;
+      const bool ok = live && fi >= 0 && fi < Fi && ti >= 0 && ti < Ti;
+      const int row = rb[i] + fi * Ti + ti;
+      ra[i] = bload4(r0, ok ? (row * ld + c + c4) * 4 : kOOB);
+    }
+    c += 32;
+    if (c >= cin) {
+      c -= cin;
+      ++j;
+    }
+  }
+};
+
+// Shared GEMM epilogue for a wave's TM x TN tiles of 32x32 accumulators
+// (gfx950 32x32 C/D map: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)).
+// Branch-free: buffer loads / stores with out-of-range offsets for rows >= M
+// (loads return 0, stores are dropped), every residual load issued before the
+// first use — no per-element exec branches and serialised round trips.
+//   y = act(acc + bias[n] + row_bias[row/T][n] + res[row][n]) * scale[n] + shift[n]
+template <int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0,
+                                              int wm, int wn, int lane) {
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
+  if (p.res) {
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + (wn * TN + j) * 32 + r32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + (wm * TM + i) * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+          const int off = row < p.M ? (row * p.ldres + col) * 4 : kOOB;
+          acc[i][j][r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, off, 0, 0));
+        }
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + (wn * TN + j) * 32 + r32;
+    const float bv = p.bias ? p.bias[col] : 0.f;
+    const float sc = p.scale ? p.scale[col] : 1.f;
+    const float sh = p.scale ? p.shift[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + (wm * TM + i) * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+        float y = acc[i][j][r] + bv;
+        if (p.row_bias) {
+          const int ub = (row < p.M ? row : p.M - 1) / p.T;
+          y += p.row_bias[(size_t)ub * p.N + col];
+        }
+        if (p.act == kActRelu) y = fmaxf(y, 0.f);
+        else if (p.act == kActTanh) y = tanhf(y);
+        y = y * sc + sh;
+        const int off = row < p.M ? (row * p.ldo + col) * 4 : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, off, 0, 0);
+      }
+    }
+  }
+}
+
 // True when every 32-wide k-tile of the operand stays in one tap and segment.
 inline bool uniform_ktiles(const ConvGemmArgs& p) {
   if (p.cin % 32 != 0) return false;
@@ -134,12 +242,20 @@ inline void check_conv_args(const ConvGemmArgs& p, const char* who) {
   // buffer-load byte offsets are 32-bit: every operand must stay below 2 GiB
   for (int i = 0; i < 3; ++i)
     WSP_CHECK((long long)p.M * p.lda[i] * 4 < (long long)kOOB, w + ": operand exceeds 2 GiB (split the batch)");
+  WSP_CHECK((long long)p.M * p.ldo * 4 < (long long)kOOB, w + ": output exceeds 2 GiB (split the batch)");
+  if (p.res) WSP_CHECK((long long)p.M * p.ldres * 4 < (long long)kOOB, w + ": residual exceeds 2 GiB");
   WSP_CHECK((long long)p.N * p.Kp * 4 < (long long)kOOB, w + ": weights exceed 2 GiB");
   WSP_CHECK(p.M > 0 && p.N > 0 && p.K > 0 && p.T > 0, w + ": empty shape");
   WSP_CHECK(p.cin % 4 == 0, w + ": cin must be a multiple of 4");
   WSP_CHECK(p.K == p.cin * p.taps, w + ": K != cin * taps");
   WSP_CHECK(p.Kp % 32 == 0 && p.Kp >= p.K, w + ": bad packed K");
-  WSP_CHECK(p.N % 64 == 0, w + ": N must be a multiple of 64");
+  WSP_CHECK(p.N % 32 == 0, w + ": N must be a multiple of 32");
+  if (p.conv2d) {
+    WSP_CHECK(p.amode == kACat && p.cseg[1] == p.cin && p.cin % 32 == 0,
+              w + ": 2-D conv needs one segment with cin % 32 == 0");
+    WSP_CHECK(p.M == p.T * p.Fo * p.To || p.T > 0, w + ": bad 2-D shape");
+    WSP_CHECK(p.taps % p.kw == 0 && p.stride >= 1, w + ": bad 2-D taps/stride");
+  }
   for (int i = 0; i < 3; ++i) WSP_CHECK(p.lda[i] % 4 == 0, w + ": lda must be a multiple of 4");
   if (p.amode == kACat) {
     WSP_CHECK(p.cseg[0] == 0 && p.cseg[3] == p.cin && p.cseg[1] <= p.cseg[2] &&

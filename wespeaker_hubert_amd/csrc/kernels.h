@@ -39,12 +39,20 @@ struct ConvGemmArgs {
   int act;
   int amode;
   int role;  // 1 = SE-Res2Block 1x1 CxC conv (own kernel symbol for profiling)
+  // 2-D (NHWC, ResNet) mode: input [B][Fi][Ti][cin], output rows m = (b*Fo + fo)*To + to,
+  // taps = kh*kw with tap j = kf*kw + kt, input (fo*stride + kf - pad, to*stride + kt - pad).
+  int conv2d;
+  int Fi, Ti, Fo, To, stride, kw;
 };
 
 // bf16x3 split-precision variant (conv_gemm_x3.hip); whi/wlo = packed [N][Kp]
 // bf16 hi/lo images of W.  variant: 0 = 128x128/4 waves, 1 = 256x128/8 waves.
 void launch_conv_gemm_x3(const ConvGemmArgs& p, const void* whi, const void* wlo, int variant,
                          hipStream_t s);
+
+// LDS-DMA staged bf16x3 variant (conv_gemm_dma.hip): kACat operands, N % 128.
+bool conv_gemm_dma_supported(const ConvGemmArgs& p);
+void launch_conv_gemm_dma(const ConvGemmArgs& p, const void* whi, const void* wlo, hipStream_t s);
 
 // tile: 0 = 128x128 block (N % 128 == 0), 1 = 128x64 block (N % 64 == 0)
 void launch_conv_gemm(const ConvGemmArgs& p, hipStream_t s);
@@ -81,6 +89,10 @@ void launch_residual_scale(const float* x, const float* h, const float* g, float
 // of logits e [B*T][C], weighted mean/std of x [B*T][C] -> out [B][2C].
 void launch_astp_pool(const float* e, const float* x, int B, int T, int C, float* out,
                       hipStream_t s);
+
+// ResNet stem: 1 -> C0 3x3 conv + folded BN + ReLU, (B,T,F) feats -> NHWC [B][F][T][C0].
+void launch_resnet_stem(const float* feats, int B, int T, int F, int C0, const float* w, const float* bias,
+                        float* out, hipStream_t s);
 
 // Kaldi fbank + optional CMN.  `tables` = device copy of fbank_tables().
 constexpr int kFbankTableFloats = 1664 + 1024;

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <string>
@@ -126,6 +127,20 @@ struct Model::Impl {
   ConvW conv, pool1, pool2;
   LinW pool1_ctx;
   LinW head;
+
+  // ResNet (resnet.py:110-260), NHWC activations [B][F][T][C]
+  bool bottleneck = true;
+  int nblocks[4] = {0, 0, 0, 0};
+  int m_ch = 32;
+  float* stem_w = nullptr;
+  float* stem_b = nullptr;
+  struct RBlock {
+    ConvW c1, c2, c3, sc;
+    bool has_sc = false;
+    int stride = 1, in_planes = 0, planes = 0, out_planes = 0;
+  };
+  std::vector<RBlock> rblocks;
+  LinW seg1;
 
   // 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA
   int precision = 1;
@@ -255,6 +270,230 @@ struct Model::Impl {
     if (emb_bn) add_bn("bn2", embed_dim);
   }
 
+  void build_resnet_params() {
+    const int exp = bottleneck ? 4 : 1;
+    add("conv1.weight", {m_ch, 1, 3, 3});
+    add_bn("bn1", m_ch);
+    int in_planes = m_ch;
+    for (int li = 0; li < 4; ++li) {
+      const int planes = m_ch << li;
+      for (int bi = 0; bi < nblocks[li]; ++bi) {
+        const int stride = (li > 0 && bi == 0) ? 2 : 1;
+        const std::string p = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+        RBlock rb;
+        rb.stride = stride;
+        rb.in_planes = in_planes;
+        rb.planes = planes;
+        rb.out_planes = planes * exp;
+        if (bottleneck) {
+          add(p + ".conv1.weight", {planes, in_planes, 1, 1});
+          add_bn(p + ".bn1", planes);
+          add(p + ".conv2.weight", {planes, planes, 3, 3});
+          add_bn(p + ".bn2", planes);
+          add(p + ".conv3.weight", {planes * 4, planes, 1, 1});
+          add_bn(p + ".bn3", planes * 4);
+        } else {
+          add(p + ".conv1.weight", {planes, in_planes, 3, 3});
+          add_bn(p + ".bn1", planes);
+          add(p + ".conv2.weight", {planes, planes, 3, 3});
+          add_bn(p + ".bn2", planes);
+        }
+        if (stride != 1 || in_planes != exp * planes) {
+          rb.has_sc = true;
+          add(p + ".shortcut.0.weight", {exp * planes, in_planes, 1, 1});
+          add_bn(p + ".shortcut.1", exp * planes);
+        }
+        rblocks.push_back(rb);
+        in_planes = planes * exp;
+      }
+    }
+    const int stats_dim = (feat_dim / 8) * m_ch * 8 * exp;
+    add("seg_1.weight", {embed_dim, stats_dim * 2});
+    add("seg_1.bias", {embed_dim});
+  }
+
+  // conv -> BN (eval) folded into the weights: W' = W * s[n], bias = shift.
+  ConvW pack_conv_bn(const std::string& wname, const std::string& bn, int N, int cin, int taps) {
+    std::vector<double> sc, sh;
+    bn_affine(bn, sc, sh);
+    std::vector<float> w = P(wname);
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < cin * taps; ++k) w[(size_t)n * cin * taps + k] = (float)(w[(size_t)n * cin * taps + k] * sc[n]);
+    std::vector<float> b(N);
+    for (int n = 0; n < N; ++n) b[n] = (float)sh[n];
+    return pack_conv(w, N, cin, taps, b.data(), "");
+  }
+
+  void finalize_resnet() {
+    {
+      std::vector<double> sc, sh;
+      bn_affine("bn1", sc, sh);
+      const auto& w = P("conv1.weight");
+      std::vector<float> wf(m_ch * 9), bf(m_ch);
+      for (int c = 0; c < m_ch; ++c) {
+        for (int q = 0; q < 9; ++q) wf[c * 9 + q] = (float)(w[c * 9 + q] * sc[c]);
+        bf[c] = (float)sh[c];
+      }
+      stem_w = dev.upload(wf);
+      stem_b = dev.upload(bf);
+    }
+    int idx_b = 0;
+    for (int li = 0; li < 4; ++li)
+      for (int bi = 0; bi < nblocks[li]; ++bi) {
+        RBlock& rb = rblocks[idx_b++];
+        const std::string p = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+        if (bottleneck) {
+          rb.c1 = pack_conv_bn(p + ".conv1.weight", p + ".bn1", rb.planes, rb.in_planes, 1);
+          rb.c2 = pack_conv_bn(p + ".conv2.weight", p + ".bn2", rb.planes, rb.planes, 9);
+          rb.c3 = pack_conv_bn(p + ".conv3.weight", p + ".bn3", rb.out_planes, rb.planes, 1);
+        } else {
+          rb.c1 = pack_conv_bn(p + ".conv1.weight", p + ".bn1", rb.planes, rb.in_planes, 9);
+          rb.c2 = pack_conv_bn(p + ".conv2.weight", p + ".bn2", rb.planes, rb.planes, 9);
+        }
+        if (rb.has_sc) rb.sc = pack_conv_bn(p + ".shortcut.0.weight", p + ".shortcut.1", rb.out_planes, rb.in_planes, 1);
+      }
+    // seg_1 over TSTP stats; reference flatten index s*C*F4 + c*F4 + f, ours f*2C + s*C + c
+    const int C4 = rblocks.back().out_planes, F4 = feat_dim / 8;
+    const auto& W = P("seg_1.weight");
+    const int K = 2 * C4 * F4;
+    std::vector<float> wp((size_t)embed_dim * K);
+    for (int n = 0; n < embed_dim; ++n)
+      for (int f = 0; f < F4; ++f)
+        for (int sidx = 0; sidx < 2; ++sidx)
+          for (int c = 0; c < C4; ++c)
+            wp[(size_t)n * K + f * 2 * C4 + sidx * C4 + c] = W[(size_t)n * K + sidx * C4 * F4 + c * F4 + f];
+    seg1 = pack_lin(wp.data(), embed_dim, K, K, P("seg_1.bias").data());
+  }
+
+  struct RShapes {
+    size_t big = 0, y1 = 0, y2 = 0, sc = 0;  // floats per utterance
+    int F4 = 0, T4 = 0, C4 = 0;
+  };
+  RShapes resnet_shapes(int T) const {
+    RShapes r;
+    int Fi = feat_dim, Ti = T;
+    r.big = (size_t)Fi * Ti * m_ch;
+    for (const RBlock& rb : rblocks) {
+      const int Fo = (Fi - 1) / rb.stride + 1, To = (Ti - 1) / rb.stride + 1;
+      r.big = std::max(r.big, (size_t)Fo * To * rb.out_planes);
+      r.y1 = std::max(r.y1, (size_t)(bottleneck ? Fi * Ti : Fo * To) * rb.planes);
+      r.y2 = std::max(r.y2, (size_t)Fo * To * rb.planes);
+      if (rb.has_sc) r.sc = std::max(r.sc, (size_t)Fo * To * rb.out_planes);
+      Fi = Fo;
+      Ti = To;
+    }
+    r.F4 = Fi;
+    r.T4 = Ti;
+    r.C4 = rblocks.back().out_planes;
+    return r;
+  }
+  // utterances per forward chunk: every activation operand must stay < 2 GiB
+  // (32-bit buffer-load offsets).
+  int resnet_chunk(int B, int T) const {
+    const RShapes r = resnet_shapes(T);
+    const size_t per = std::max(r.big, std::max(r.y1, std::max(r.y2, r.sc))) * sizeof(float);
+    int bc = (int)std::max<size_t>(1, ((size_t)1 << 31) / 8 * 7 / per);
+    bc = std::min(bc, B);
+    const int chunks = (B + bc - 1) / bc;
+    return (B + chunks - 1) / chunks;
+  }
+  size_t resnet_ws_floats(int B, int T, size_t* offs) const {
+    const int bc = resnet_chunk(B, T);
+    const RShapes r = resnet_shapes(T);
+    const size_t sizes[] = {bc * r.big, bc * r.big, bc * r.y1, bc * r.y2, bc * std::max<size_t>(r.sc, 1),
+                            (size_t)bc * r.F4 * 2 * r.C4};
+    size_t o = 0;
+    for (int i = 0; i < 6; ++i) {
+      if (offs) offs[i] = o;
+      o += (sizes[i] + 63) / 64 * 64;
+    }
+    return o;
+  }
+
+  void gemm2d(const char* tag, const ConvW& cw, const float* a0, int lda, float* out, int ldo, int B,
+              int Fi, int Ti, int kw, int stride, int pad, int act, const float* res, int ldres,
+              hipStream_t s) {
+    ConvGemmArgs g{};
+    g.a[0] = g.a[1] = g.a[2] = a0;
+    g.lda[0] = g.lda[1] = g.lda[2] = lda;
+    g.cseg[0] = 0;
+    g.cseg[1] = g.cseg[2] = g.cseg[3] = cw.cin;
+    const int Fo = (Fi + 2 * pad - kw) / stride + 1, To = (Ti + 2 * pad - kw) / stride + 1;
+    const int M = B * Fo * To;
+    fill(g, cw, M, M, 1, pad, out, ldo, act, nullptr, true);
+    g.conv2d = 1;
+    g.Fi = Fi;
+    g.Ti = Ti;
+    g.Fo = Fo;
+    g.To = To;
+    g.stride = stride;
+    g.kw = kw;
+    g.res = res;
+    g.ldres = ldres;
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, 1, s); });
+  }
+  void gemm1x1(const char* tag, const ConvW& cw, const float* a0, float* out, int M, int act, const float* res,
+               hipStream_t s) {
+    ConvGemmArgs g{};
+    g.a[0] = g.a[1] = g.a[2] = a0;
+    g.lda[0] = g.lda[1] = g.lda[2] = cw.cin;
+    g.cseg[0] = 0;
+    g.cseg[1] = g.cseg[2] = g.cseg[3] = cw.cin;
+    fill(g, cw, M, M, 1, 0, out, cw.N, act, nullptr, true);
+    g.res = res;
+    g.ldres = cw.N;
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, 1, s); });
+  }
+
+  void forward_resnet(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
+    const int bc = resnet_chunk(B, T);
+    size_t off[6];
+    resnet_ws_floats(B, T, off);
+    float* X = ws + off[0];
+    float* O = ws + off[1];
+    float* Y1 = ws + off[2];
+    float* Y2 = ws + off[3];
+    float* SC = ws + off[4];
+    float* pooled = ws + off[5];
+    for (int b0 = 0; b0 < B; b0 += bc) {
+      const int nb = std::min(bc, B - b0);
+      int Fi = feat_dim, Ti = T, Ci = m_ch;
+      run("stem", 0, s, [&] {
+        launch_resnet_stem(feats + (size_t)b0 * T * feat_dim, nb, T, feat_dim, m_ch, stem_w, stem_b, X, s);
+      });
+      float* x = X;
+      float* o = O;
+      for (const RBlock& rb : rblocks) {
+        const int Fo = (Fi - 1) / rb.stride + 1, To = (Ti - 1) / rb.stride + 1;
+        const float* res = x;
+        if (rb.has_sc) {
+          gemm2d("shortcut", rb.sc, x, Ci, SC, rb.out_planes, nb, Fi, Ti, 1, rb.stride, 0, kActNone, nullptr, 0, s);
+          res = SC;
+        }
+        if (bottleneck) {
+          gemm1x1("res_conv1x1", rb.c1, x, Y1, nb * Fi * Ti, kActRelu, nullptr, s);
+          gemm2d("res_conv3x3", rb.c2, Y1, rb.planes, Y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
+          gemm1x1("res_conv1x1", rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
+        } else {
+          gemm2d("res_conv3x3", rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
+          gemm2d("res_conv3x3", rb.c2, Y1, rb.planes, o, rb.out_planes, nb, Fo, To, 3, 1, 1, kActRelu, res,
+                 rb.out_planes, s);
+        }
+        std::swap(x, o);
+        Fi = Fo;
+        Ti = To;
+        Ci = rb.out_planes;
+      }
+      // TSTP over frames for every (utterance, freq) row block, then seg_1
+      run("tstp_head", 0, s, [&] {
+        launch_frame_stats(x, Ci, nb * Fi, Ti, Ci, pooled, 2 * Ci, 1, Ci, s);
+        launch_small_linear({pooled, Fi * 2 * Ci, seg1.wt, seg1.bias, embed + (size_t)b0 * embed_dim, embed_dim, nb,
+                             Fi * 2 * Ci, embed_dim, 0},
+                            s);
+      });
+    }
+  }
+
   void finalize_ecapa() {
     const int w = C / 8;
     layer1 = pack_conv(P("layer1.conv.weight"), C, feat_dim, 5, P("layer1.conv.bias").data(), "layer1.bn");
@@ -343,8 +582,10 @@ struct Model::Impl {
     run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch(g, cw, s); });
   }
   void launch(const ConvGemmArgs& g, const ConvW& cw, hipStream_t s) {
-    if (precision == 1)
-      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant, s);
+    if (precision == 1 && x3_variant == 2 && conv_gemm_dma_supported(g))
+      launch_conv_gemm_dma(g, cw.whi, cw.wlo, s);
+    else if (precision == 1)
+      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 1 : x3_variant, s);
     else
       launch_conv_gemm(g, s);
   }
@@ -504,6 +745,20 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
     WSP_CHECK(feat_dim > 0 && feat_dim % 4 == 0, "ECAPA feat_dim must be a positive multiple of 4");
     WSP_CHECK(embed_dim > 0, "embed_dim must be positive");
     m.build_ecapa_params();
+  } else if (arch.rfind("ResNet", 0) == 0) {
+    static const std::map<std::string, std::pair<bool, std::vector<int>>> kRes = {
+        {"ResNet18", {false, {2, 2, 2, 2}}},     {"ResNet34", {false, {3, 4, 6, 3}}},
+        {"ResNet50", {true, {3, 4, 6, 3}}},      {"ResNet101", {true, {3, 4, 23, 3}}},
+        {"ResNet152", {true, {3, 8, 36, 3}}},    {"ResNet221", {true, {6, 16, 48, 3}}},
+        {"ResNet293", {true, {10, 20, 64, 3}}}};
+    auto it = kRes.find(arch);
+    WSP_CHECK(it != kRes.end(), "unsupported arch " + arch);
+    WSP_CHECK(!two_emb, "ResNet two_emb_layer=True is not implemented");
+    WSP_CHECK(feat_dim >= 8, "ResNet feat_dim must be >= 8");
+    m.ecapa = false;
+    m.bottleneck = it->second.first;
+    for (int i = 0; i < 4; ++i) m.nblocks[i] = it->second.second[i];
+    m.build_resnet_params();
   } else {
     throw InvalidArg{"unsupported arch " + arch};
   }
@@ -536,7 +791,10 @@ void Model::finalize() {
   for (auto& p : m.params)
     WSP_CHECK(p.set || p.name.find("num_batches_tracked") != std::string::npos,
               "parameter not set: " + p.name);
-  m.finalize_ecapa();
+  if (m.ecapa)
+    m.finalize_ecapa();
+  else
+    m.finalize_resnet();
   for (auto& p : m.params) std::vector<float>().swap(p.host);
   m.finalized = true;
 }
@@ -545,7 +803,8 @@ int Model::embed_dim() const { return impl->embed_dim; }
 int Model::feat_dim() const { return impl->feat_dim; }
 
 size_t Model::workspace_bytes(int B, int T) const {
-  return impl->ecapa_ws_floats(B, T, nullptr) * sizeof(float) + 256;
+  const size_t f = impl->ecapa ? impl->ecapa_ws_floats(B, T, nullptr) : impl->resnet_ws_floats(B, T, nullptr);
+  return f * sizeof(float) + 256;
 }
 
 void Model::forward(const float* feats, int B, int T, float* embed, void* ws, size_t ws_bytes,
@@ -556,7 +815,12 @@ void Model::forward(const float* feats, int B, int T, float* embed, void* ws, si
   WSP_CHECK((size_t)B * T < (1u << 31), "B*T too large");
   WSP_CHECK(ws_bytes >= workspace_bytes(B, T), "workspace too small");
   float* wsf = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
-  m.forward_ecapa(feats, B, T, embed, wsf, s);
+  if (m.ecapa) {
+    m.forward_ecapa(feats, B, T, embed, wsf, s);
+  } else {
+    WSP_CHECK(m.precision == 1, "ResNet runs on the bf16x3 kernels only (precision=1)");
+    m.forward_resnet(feats, B, T, embed, wsf, s);
+  }
 }
 
 void Model::profile(bool on) { impl->prof = on; }
@@ -566,7 +830,7 @@ void Model::set_option(const std::string& key, int value) {
     WSP_CHECK(value == 0 || value == 1, "precision must be 0 (f32) or 1 (bf16x3)");
     impl->precision = value;
   } else if (key == "x3_variant") {
-    WSP_CHECK(value == 0 || value == 1, "x3_variant must be 0 or 1");
+    WSP_CHECK(value >= 0 && value <= 2, "x3_variant must be 0, 1 or 2");
     impl->x3_variant = value;
   } else {
     throw InvalidArg{"unknown option " + key};

@@ -6,58 +6,59 @@
 namespace wsp {
 
 // ----------------------------------------------------------- small linear ---
-// out[r][n] = post(act(bias[n] + sum_k in[r][k] * wt[k][n])).  One workgroup =
-// kRB rows x 256 outputs; the kRB input rows are staged through LDS in 256-wide
-// k chunks, the weight column is read coalesced (wt is k-major).
+// out[r][n] = act(bias[n] + sum_k in[r][k] * wt[k][n]) for the row-batched
+// GEMVs (SE FCs, GLOB context bias, BN-folded embedding head): R = batch rows,
+// K <= a few thousand.  One workgroup = kRB rows x 64 outputs (lane = output,
+// coalesced k-major weight reads); the 4 waves split K and reduce through LDS.
+// Input rows are wave-uniform (scalar loads).
 namespace {
-constexpr int kRB = 8;
-constexpr int kKC = 256;
+constexpr int kRB = 4;
 
 __global__ __launch_bounds__(256) void small_linear_kernel(const SmallLinearArgs p) {
-  __shared__ float s_in[kRB][kKC];
-  const int tid = threadIdx.x;
-  const int n = blockIdx.y * 256 + tid;
+  __shared__ float part[4][kRB][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int n = blockIdx.y * 64 + lane;
   const int r0 = blockIdx.x * kRB;
+  const int kq = (p.K + 3) / 4;
+  const int k0 = wave * kq, k1 = min(p.K, k0 + kq);
   float acc[kRB];
 #pragma unroll
   for (int r = 0; r < kRB; ++r) acc[r] = 0.f;
-  for (int k0 = 0; k0 < p.K; k0 += kKC) {
-    const int kc = min(kKC, p.K - k0);
-    for (int i = tid; i < kRB * kKC; i += 256) {
-      const int r = i / kKC, k = i - r * kKC;
-      s_in[r][k] = (r0 + r < p.R && k < kc) ? p.in[(long)(r0 + r) * p.ldin + k0 + k] : 0.f;
-    }
-    __syncthreads();
-    if (n < p.N) {
-      const float* w = p.wt + (long)k0 * p.N + n;
-      int k = 0;
-      for (; k + 4 <= kc; k += 4) {
-        const float w0 = w[(long)k * p.N], w1 = w[(long)(k + 1) * p.N];
-        const float w2 = w[(long)(k + 2) * p.N], w3 = w[(long)(k + 3) * p.N];
+  const float* in[kRB];
 #pragma unroll
-        for (int r = 0; r < kRB; ++r) {
-          float a = acc[r];
-          a = fmaf(s_in[r][k], w0, a);
-          a = fmaf(s_in[r][k + 1], w1, a);
-          a = fmaf(s_in[r][k + 2], w2, a);
-          a = fmaf(s_in[r][k + 3], w3, a);
-          acc[r] = a;
-        }
-      }
-      for (; k < kc; ++k) {
-        const float w0 = w[(long)k * p.N];
-#pragma unroll
-        for (int r = 0; r < kRB; ++r) acc[r] = fmaf(s_in[r][k], w0, acc[r]);
-      }
-    }
-    __syncthreads();
-  }
+  for (int r = 0; r < kRB; ++r) in[r] = p.in + (long)min(r0 + r, p.R - 1) * p.ldin;
   if (n < p.N) {
+    const float* w = p.wt + n;
+    int k = k0;
+    for (; k + 4 <= k1; k += 4) {
+      const float w0 = w[(long)k * p.N], w1 = w[(long)(k + 1) * p.N];
+      const float w2 = w[(long)(k + 2) * p.N], w3 = w[(long)(k + 3) * p.N];
+#pragma unroll
+      for (int r = 0; r < kRB; ++r) {
+        float a = acc[r];
+        a = fmaf(in[r][k], w0, a);
+        a = fmaf(in[r][k + 1], w1, a);
+        a = fmaf(in[r][k + 2], w2, a);
+        a = fmaf(in[r][k + 3], w3, a);
+        acc[r] = a;
+      }
+    }
+    for (; k < k1; ++k) {
+      const float w0 = w[(long)k * p.N];
+#pragma unroll
+      for (int r = 0; r < kRB; ++r) acc[r] = fmaf(in[r][k], w0, acc[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kRB; ++r) part[wave][r][lane] = acc[r];
+  __syncthreads();
+  if (wave == 0 && n < p.N) {
     const float bv = p.bias ? p.bias[n] : 0.f;
 #pragma unroll
     for (int r = 0; r < kRB; ++r) {
       if (r0 + r >= p.R) break;
-      float y = acc[r] + bv;
+      float y = ((part[0][r][lane] + part[1][r][lane]) + (part[2][r][lane] + part[3][r][lane])) + bv;
       if (p.act == 1) y = fmaxf(y, 0.f);
       else if (p.act == 2) y = tanhf(y);
       else if (p.act == 3) y = 1.f / (1.f + expf(-y));
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(256) void small_linear_kernel(const SmallLinearArgs
 
 void launch_small_linear(const SmallLinearArgs& p, hipStream_t s) {
   if (p.R == 0) return;
-  dim3 grid(ceil_div(p.R, kRB), ceil_div(p.N, 256));
+  dim3 grid(ceil_div(p.R, kRB), ceil_div(p.N, 64));
   hipLaunchKernelGGL(small_linear_kernel, grid, dim3(256), 0, s, p);
   WSP_HIP(hipGetLastError());
 }
@@ -217,6 +218,69 @@ void launch_astp_pool(const float* e, const float* x, int B, int T, int C, float
   if (B == 0) return;
   dim3 grid(B, ceil_div(C, 64));
   hipLaunchKernelGGL(astp_pool_kernel, grid, dim3(256), 0, s, e, x, T, C, out);
+  WSP_HIP(hipGetLastError());
+}
+
+}  // namespace wsp
+
+namespace wsp {
+
+// ------------------------------------------------------------ ResNet stem ---
+// conv1 of the r-vector ResNet (resnet.py:130-136,174-176): 1 -> C0 channels,
+// 3x3, pad 1, BN folded into (w, bias), ReLU.  Input = the reference's (B,T,F)
+// features read as the (B,1,F,T) image; output NHWC [B][F][T][C0].
+namespace {
+template <int C0>
+__global__ __launch_bounds__(256) void resnet_stem_kernel(const float* __restrict__ feats, int T, int F,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out, long total) {
+  __shared__ float s_w[C0 * 9];
+  __shared__ float s_b[C0];
+  for (int i = threadIdx.x; i < C0 * 9; i += 256) s_w[i] = w[i];
+  for (int i = threadIdx.x; i < C0; i += 256) s_b[i] = bias[i];
+  __syncthreads();
+  const long idx = blockIdx.x * 256L + threadIdx.x;
+  if (idx >= total) return;
+  const int t = (int)(idx % T);
+  const long bf = idx / T;
+  const int f = (int)(bf % F);
+  const int b = (int)(bf / F);
+  float x[9];
+#pragma unroll
+  for (int kf = 0; kf < 3; ++kf)
+#pragma unroll
+    for (int kt = 0; kt < 3; ++kt) {
+      const int ff = f + kf - 1, tt = t + kt - 1;
+      x[kf * 3 + kt] = (ff >= 0 && ff < F && tt >= 0 && tt < T) ? feats[((long)b * T + tt) * F + ff] : 0.f;
+    }
+  f32x4* o = reinterpret_cast<f32x4*>(out + idx * C0);
+#pragma unroll
+  for (int c4 = 0; c4 < C0 / 4; ++c4) {
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = c4 * 4 + e;
+      float a = s_b[c];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) a = fmaf(x[q], s_w[c * 9 + q], a);
+      v[e] = fmaxf(a, 0.f);
+    }
+    o[c4] = v;
+  }
+}
+}  // namespace
+
+void launch_resnet_stem(const float* feats, int B, int T, int F, int C0, const float* w, const float* bias,
+                        float* out, hipStream_t s) {
+  WSP_CHECK(C0 == 32 || C0 == 64, "resnet stem: m_channels must be 32 or 64");
+  const long total = (long)B * F * T;
+  if (total == 0) return;
+  const unsigned grid = (unsigned)((total + 255) / 256);
+  if (C0 == 32)
+    hipLaunchKernelGGL(resnet_stem_kernel<32>, dim3(grid), dim3(256), 0, s, feats, T, F, w, bias, out, total);
+  else
+    hipLaunchKernelGGL(resnet_stem_kernel<64>, dim3(grid), dim3(256), 0, s, feats, T, F, w, bias, out, total);
   WSP_HIP(hipGetLastError());
 }
 

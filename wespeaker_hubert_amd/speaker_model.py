@@ -30,13 +30,12 @@ def _to_numpy(v) -> np.ndarray:
 
 
 class HipSpeakerModel:
-    """ECAPA-TDNN speaker backbone executed by hand-written gfx950 kernels."""
+    """ECAPA-TDNN / ResNet speaker backbone executed by hand-written gfx950 kernels."""
 
     def __init__(self, arch: str, **model_args):
         self.spec: ModelSpec = make_spec(arch, **model_args)
-        if self.spec.family != "ecapa":
-            raise NotImplementedError(f"{arch}: the HIP runtime implements the ECAPA-TDNN family "
-                                      "in this build (ResNet is oracle/parity-fixture only)")
+        if self.spec.two_emb_layer:
+            raise NotImplementedError("two_emb_layer=True is not implemented on the HIP path")
         self._layout = param_list(self.spec)
         self._host: Dict[str, np.ndarray] = {}
         self._handle: Optional[ctypes.c_void_p] = None
