@@ -155,3 +155,51 @@ def ecapa_gflop_per_utt(spec: ModelSpec, T: int) -> float:
     macs += 128 * 1536 * T                                  # pool.linear2
     macs += 3072 * spec.embed_dim
     return 2.0 * macs / 1e9
+
+
+# ---------------------------------------------------------------- HuBERT ---
+# s3prl HuBERT-base upstream as wrapped by wespeaker/frontend/s3prl.py:23-93.
+# Canonical keys are the fairseq names s3prl loads, under the prefix the
+# reference checkpoint uses (`model.add_module("frontend", ...)`,
+# bin/extract.py:49-55 -> S3PRLUpstream.upstream.model).
+HUBERT_PREFIX = "frontend.upstream.upstream.model."
+HUBERT_BASE = dict(conv_dim=512, conv_kernel=(10, 3, 3, 3, 3, 2, 2), conv_stride=(5, 2, 2, 2, 2, 2, 2),
+                   hidden=768, layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16)
+
+
+def hubert_params(cfg=HUBERT_BASE, prefix: str = HUBERT_PREFIX) -> ParamList:
+    c, h = cfg["conv_dim"], cfg["hidden"]
+    out: ParamList = []
+    for i, k in enumerate(cfg["conv_kernel"]):
+        out.append((f"feature_extractor.conv_layers.{i}.0.weight", (c, 1 if i == 0 else c, k)))
+        if i == 0:
+            out += [("feature_extractor.conv_layers.0.2.weight", (c,)),
+                    ("feature_extractor.conv_layers.0.2.bias", (c,))]
+    out += [("layer_norm.weight", (c,)), ("layer_norm.bias", (c,)),
+            ("post_extract_proj.weight", (h, c)), ("post_extract_proj.bias", (h,)),
+            ("encoder.pos_conv.0.bias", (h,)), ("encoder.pos_conv.0.weight_g", (1, 1, cfg["pos_k"])),
+            ("encoder.pos_conv.0.weight_v", (h, h // cfg["pos_groups"], cfg["pos_k"])),
+            ("encoder.layer_norm.weight", (h,)), ("encoder.layer_norm.bias", (h,))]
+    for li in range(cfg["layers"]):
+        p = f"encoder.layers.{li}."
+        for proj in ("k_proj", "v_proj", "q_proj", "out_proj"):
+            out += [(p + f"self_attn.{proj}.weight", (h, h)), (p + f"self_attn.{proj}.bias", (h,))]
+        out += [(p + "self_attn_layer_norm.weight", (h,)), (p + "self_attn_layer_norm.bias", (h,)),
+                (p + "fc1.weight", (cfg["ffn"], h)), (p + "fc1.bias", (cfg["ffn"],)),
+                (p + "fc2.weight", (h, cfg["ffn"])), (p + "fc2.bias", (h,)),
+                (p + "final_layer_norm.weight", (h,)), (p + "final_layer_norm.bias", (h,))]
+    out = [(prefix + n, s) for n, s in out]
+    out.append(("frontend.featurizer.weights", (cfg["layers"] + 1,)))
+    return out
+
+
+def hubert_num_frames(num_samples: int, cfg=HUBERT_BASE) -> int:
+    t = num_samples
+    for k, s in zip(cfg["conv_kernel"], cfg["conv_stride"]):
+        t = (t - k) // s + 1
+    return t
+
+
+def s3prl_num_frames(num_samples: int, downsample_rate: int = 320) -> int:
+    """len(range(0, W, 320)) — s3prl's length match target."""
+    return (num_samples + downsample_rate - 1) // downsample_rate

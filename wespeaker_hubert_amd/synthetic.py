@@ -35,6 +35,10 @@ def synth_param(seed: int, name: str, shape: Tuple[int, ...]) -> np.ndarray:
         return (0.1 * rng.standard_normal(shape)).astype(np.float32)
     if leaf == "running_var":
         return rng.uniform(0.5, 1.5, shape).astype(np.float32)
+    if leaf == "weight_g":  # weight-norm magnitude (HuBERT pos_conv): per-tap norms
+        return rng.uniform(1.5, 3.0, shape).astype(np.float32)
+    if name.endswith("featurizer.weights"):
+        return (0.5 * rng.standard_normal(shape)).astype(np.float32)
     is_norm = (".bn" in name or name.startswith("bn") or ".norm" in name
                or "layer_norm" in name or "bns." in name or "seg_bn" in name)
     if leaf == "weight" and len(shape) == 1:
