@@ -30,9 +30,9 @@ from wespeaker_hubert_amd.synthetic import synth_audio, synth_state_dict  # noqa
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (no sparsity)
 HBM_PEAK_GBPS = 8000.0
-DOMINANT = {  # kernel symbol of the SE-Res2Block 1x1 CxC conv (ConvGemmArgs.role == 1)
-    1: "_ZN3wsp12_GLOBAL__N_112conv_gemm_x3ILi4ELi2ELi2ELi2ELi0ELb1ELi1EEEvNS_12ConvGemmArgsEPKDF16bS4_",
-    0: "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1EEEvNS_12ConvGemmArgsE",
+DOMINANT = {  # kernel-symbol prefix of the SE-Res2Block 1x1 CxC conv (ConvGemmArgs.role == 1)
+    1: "_ZN3wsp12_GLOBAL__N_112conv_gemm_x3ILi4ELi2ELi2ELi2ELi0ELb1ELi1E",
+    0: "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1E",
 }
 
 
@@ -43,9 +43,10 @@ def profiled_traffic(symbol: str, grid: int):
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), key=os.path.getmtime)
     for f in reversed(files):
         d = json.load(open(f))
-        v = d.get(f"{symbol}|{grid}")
-        if v:
-            return v["hbm_bytes"], os.path.basename(f)
+        for key, v in d.items():
+            sym, _, g = key.rpartition("|")
+            if sym.startswith(symbol) and g == str(grid) and v.get("hbm_bytes"):
+                return v["hbm_bytes"], os.path.basename(f) + ":" + sym
     return None, None
 
 

@@ -54,6 +54,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(const ConvGemmArgs p) {
   const int c4 = (tid & 7) * 4;
   ALoader<AR, AMODE, UNI> al;
   al.init(p, m0, srow, 32, c4);
+  if (p.gcols) al.a0 += (n0 / p.gcols) * p.gcin;  // grouped conv: this block's input channels
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w);
   int woff[BR];
 #pragma unroll
@@ -148,10 +149,12 @@ void launch_tile(const ConvGemmArgs& p, hipStream_t s) {
 
 int conv_gemm_tile_for(int N) { return (N % 128 == 0) ? 0 : 1; }
 
-void launch_conv_gemm(const ConvGemmArgs& p, hipStream_t s) {
+void launch_conv_gemm(const ConvGemmArgs& args, hipStream_t s) {
+  const ConvGemmArgs p = normalized(args);
   check_conv_args(p, "conv_gemm");
   WSP_CHECK(!p.conv2d && p.N % 64 == 0, "conv_gemm (f32): 1-D convs with N % 64 == 0 only");
-  if (conv_gemm_tile_for(p.N) == 0)
+  WSP_CHECK(!p.gcols || p.gcols % 64 == 0, "conv_gemm (f32): grouped columns must be a multiple of 64");
+  if (conv_gemm_tile_for(p.N) == 0 && !p.gcols)
     launch_tile<2, 2, 2, 2>(p, s);
   else
     launch_tile<4, 1, 1, 2>(p, s);

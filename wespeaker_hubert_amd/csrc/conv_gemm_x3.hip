@@ -64,6 +64,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   const int c4 = (tid & 7) * 4;
   std::conditional_t<C2D, ALoader2D<AR>, ALoader<AR, AMODE, UNI>> al;
   al.init(p, m0, srow, ROWS_A, c4);
+  if (p.gcols) al.a0 += (n0 / p.gcols) * p.gcin;  // grouped conv: this block's input channels
   // ---- W staging geometry: 16-B chunk id q = tid + NT*i over both images
   // (BN*4 chunks each; image = q / (BN*4) is wave-uniform), row = (q % (BN*4)) >> 2
   const __amdgpu_buffer_rsrc_t rwhi = make_rsrc(whi);
@@ -217,14 +218,17 @@ void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo,
 
 }  // namespace
 
-void launch_conv_gemm_x3(const ConvGemmArgs& p, const void* whi, const void* wlo, int variant,
+void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* wlo, int variant,
                          hipStream_t s) {
+  const ConvGemmArgs p = normalized(args);
   check_conv_args(p, "conv_gemm_x3");
   WSP_CHECK(p.Kp % 64 == 0, "conv_gemm_x3: packed K must be a multiple of 64");
   const __bf16* h = static_cast<const __bf16*>(whi);
   const __bf16* l = static_cast<const __bf16*>(wlo);
-  if (p.N % 64 != 0) {
+  if (p.N % 64 != 0 || (p.gcols && p.gcols % 64 != 0)) {
     launch_x3_tile<4, 1, 1, 1>(p, h, l, s);  // 128 x 32, 4 waves
+  } else if (p.gcols) {
+    launch_x3_tile<4, 1, 1, 2>(p, h, l, s);  // grouped: blocks stay inside one group
   } else if (p.N % 128 != 0) {
     launch_x3_tile<4, 1, 1, 2>(p, h, l, s);  // 128 x 64, 4 waves
   } else if (variant == 1) {

@@ -9,6 +9,8 @@
 // own k (single segment only).
 #pragma once
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace wsp {
@@ -37,9 +39,9 @@ struct ALoader {
   const float* a1;
   const float* a2;
   int ld0, ld1, ld2, cs1, cs2;
-  int cin, dil, pad, T, K;
+  int cin, dil, pad, Ti, K;
   int c4;
-  int a_m[AR], a_t[AR];
+  int a_r[AR], a_t[AR];  // input row / frame of tap 0 (before dil/pad)
   int j, c;  // UNI: tap and channel of the current k-tile start
 
   __device__ __forceinline__ void init(const ConvGemmArgs& p, int m0, int srow, int rows_step,
@@ -55,7 +57,7 @@ struct ALoader {
     cin = p.cin;
     dil = p.dil;
     pad = p.pad;
-    T = p.T;
+    Ti = p.Ti;
     K = p.K;
     c4 = c4_;
     j = 0;
@@ -63,8 +65,10 @@ struct ALoader {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int m = m0 + srow + rows_step * i;
-      a_m[i] = m;
-      a_t[i] = (m < p.M) ? (m % p.T) : -0x40000000;  // invalid rows fail the t-range test
+      const int b = m / p.T;
+      const int t = (m - b * p.T) * p.stride;
+      a_r[i] = b * p.Ti + t;
+      a_t[i] = (m < p.M) ? t : -0x40000000;  // invalid rows fail the t-range test
     }
   }
 
@@ -92,8 +96,8 @@ struct ALoader {
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const int tt = a_t[i] + off;
-        const bool ok = live && tt >= 0 && tt < T;
-        const int row = a_m[i] + off;
+        const bool ok = live && tt >= 0 && tt < Ti;
+        const int row = a_r[i] + off;
         ra[i] = bload4(r0, ok ? (row * ld + cl + c4) * 4 : kOOB);
         if (AMODE == kAAdd) ra[i] += bload4(r1, ok ? (row * ld1 + c + c4) * 4 : kOOB);
       }
@@ -113,8 +117,8 @@ struct ALoader {
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const int tt = a_t[i] + off;
-        const bool ok = live && kin && tt >= 0 && tt < T;
-        const int row = a_m[i] + off;
+        const bool ok = live && kin && tt >= 0 && tt < Ti;
+        const int row = a_r[i] + off;
         ra[i] = bload4(r0, ok ? (row * ld0 + cc) * 4 : kOOB);
         if (AMODE == kAAdd) ra[i] += bload4(r1, ok ? (row * ld1 + cc) * 4 : kOOB);
       }
@@ -222,6 +226,7 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
         }
         if (p.act == kActRelu) y = fmaxf(y, 0.f);
         else if (p.act == kActTanh) y = tanhf(y);
+        else if (p.act == kActGelu) y = 0.5f * y * (1.f + erff(y * 0.70710678118654752f));
         y = y * sc + sh;
         const int off = row < p.M ? (row * p.ldo + col) * 4 : kOOB;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, off, 0, 0);
@@ -240,8 +245,11 @@ inline bool uniform_ktiles(const ConvGemmArgs& p) {
 inline void check_conv_args(const ConvGemmArgs& p, const char* who) {
   const std::string w(who);
   // buffer-load byte offsets are 32-bit: every operand must stay below 2 GiB
+  // input rows: 1-D strided convs read (M / T) * Ti rows; 2-D reads B*Fi*Ti
+  const long long in_rows = p.conv2d ? (long long)(p.M / (p.Fo * p.To)) * p.Fi * p.Ti
+                                     : std::max<long long>(p.M, (long long)((p.M + p.T - 1) / p.T) * p.Ti);
   for (int i = 0; i < 3; ++i)
-    WSP_CHECK((long long)p.M * p.lda[i] * 4 < (long long)kOOB, w + ": operand exceeds 2 GiB (split the batch)");
+    WSP_CHECK(in_rows * p.lda[i] * 4 < (long long)kOOB, w + ": operand exceeds 2 GiB (split the batch)");
   WSP_CHECK((long long)p.M * p.ldo * 4 < (long long)kOOB, w + ": output exceeds 2 GiB (split the batch)");
   if (p.res) WSP_CHECK((long long)p.M * p.ldres * 4 < (long long)kOOB, w + ": residual exceeds 2 GiB");
   WSP_CHECK((long long)p.N * p.Kp * 4 < (long long)kOOB, w + ": weights exceed 2 GiB");
@@ -257,6 +265,12 @@ inline void check_conv_args(const ConvGemmArgs& p, const char* who) {
     WSP_CHECK(p.taps % p.kw == 0 && p.stride >= 1, w + ": bad 2-D taps/stride");
   }
   for (int i = 0; i < 3; ++i) WSP_CHECK(p.lda[i] % 4 == 0, w + ": lda must be a multiple of 4");
+  if (!p.conv2d) WSP_CHECK(p.stride >= 1 && p.Ti >= 1, w + ": call normalized() first");
+  if (p.gcols) {
+    WSP_CHECK(p.amode == kACat && p.cseg[1] == p.cin && !p.conv2d, w + ": grouped conv needs one 1-D segment");
+    WSP_CHECK(p.N % p.gcols == 0 && p.gcols % 32 == 0 && p.gcin % 4 == 0, w + ": bad grouped-conv columns");
+    WSP_CHECK(p.res == nullptr, w + ": grouped conv has no residual epilogue");
+  }
   if (p.amode == kACat) {
     WSP_CHECK(p.cseg[0] == 0 && p.cseg[3] == p.cin && p.cseg[1] <= p.cseg[2] &&
                   p.cseg[2] <= p.cseg[3],

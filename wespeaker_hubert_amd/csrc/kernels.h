@@ -18,7 +18,7 @@ namespace wsp {
 // epi(y) = ((y + bias[n] + row_bias[b][n] + res[m][n]) -> act) * scale[n] + shift[n]
 // ---------------------------------------------------------------------------
 enum AMode { kACat = 0, kAAdd = 1 };
-enum Act { kActNone = 0, kActRelu = 1, kActTanh = 2 };
+enum Act { kActNone = 0, kActRelu = 1, kActTanh = 2, kActGelu = 3 };  // GELU: exact erf form
 
 struct ConvGemmArgs {
   const float* a[3];
@@ -43,7 +43,22 @@ struct ConvGemmArgs {
   // taps = kh*kw with tap j = kf*kw + kt, input (fo*stride + kf - pad, to*stride + kt - pad).
   int conv2d;
   int Fi, Ti, Fo, To, stride, kw;
+  // 1-D strided conv (HuBERT feature extractor): rows m = b*T + t read input
+  // frame t*stride + j*dil - pad of [b][Ti]; stride 0 -> 1, Ti 0 -> T.
+  // Grouped conv (HuBERT pos_conv): output columns are grouped gcols wide
+  // (a block never straddles a group) and group g reads input channels
+  // [g*gcin, g*gcin + cin).  gcols 0 = ungrouped.
+  int gcols, gcin;
 };
+
+// Fills the 1-D defaults (stride 1, Ti = T) of a zero-initialised ConvGemmArgs.
+inline ConvGemmArgs normalized(ConvGemmArgs p) {
+  if (!p.conv2d) {
+    if (p.stride <= 0) p.stride = 1;
+    if (p.Ti <= 0) p.Ti = p.T;
+  }
+  return p;
+}
 
 // bf16x3 split-precision variant (conv_gemm_x3.hip); whi/wlo = packed [N][Kp]
 // bf16 hi/lo images of W.  variant: 0 = 128x128/4 waves, 1 = 256x128/8 waves.
