@@ -22,8 +22,9 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from wespeaker_hubert_amd.arch import ecapa_gflop_per_utt, make_spec  # noqa: E402
+from wespeaker_hubert_amd.arch import ecapa_gflop_per_utt, hubert_gflop_per_utt, make_spec  # noqa: E402
 from wespeaker_hubert_amd.frontend import compute_fbank  # noqa: E402
+from wespeaker_hubert_amd.s3prl_frontend import S3prlFrontend  # noqa: E402
 from wespeaker_hubert_amd.speaker_model import HipSpeakerModel  # noqa: E402
 from wespeaker_hubert_amd.synthetic import synth_audio, synth_state_dict  # noqa: E402
 
@@ -34,6 +35,15 @@ DOMINANT = {  # kernel-symbol prefix of the SE-Res2Block 1x1 CxC conv (ConvGemmA
     1: "_ZN3wsp12_GLOBAL__N_112conv_gemm_x3ILi4ELi2ELi2ELi2ELi0ELb1ELi1E",
     0: "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1E",
 }
+DOMINANT_GEMM = {  # plain (role 0) 1-D GEMM: the HuBERT FFN fc1 (M = B*T, N = 3072, K = 768)
+    1: "_ZN3wsp12_GLOBAL__N_112conv_gemm_x3ILi4ELi2ELi2ELi2ELi0ELb1ELi0ELb0E",
+    0: "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1E",
+}
+HUBERT_ARCH = "HuBERT_ECAPA_GLOB_c512"  # C4: HuBERT-base front end + ECAPA_TDNN_GLOB_c512(feat_dim 768)
+HEAD_TAGS = ("layer1", "conv1x1_CxC", "res2_k3", "se", "conv_cat", "glob_ctx", "pool_linear1", "pool_linear2",
+             "astp", "head", "stem", "shortcut", "res_conv1x1", "res_conv3x3", "tstp_head")
+HUBERT_TAGS = ("h_conv0", "h_cnn", "h_ln", "h_proj", "h_pos_conv", "h_qkv", "h_attn", "h_out_proj", "h_fc1",
+               "h_fc2", "h_cmn")
 
 
 def profiled_traffic(symbol: str, grid: int):
@@ -55,8 +65,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--arch", default="ECAPA_TDNN_c1024")
+    ap.add_argument("--batch", type=int, default=None, help="per GPU (default 256 ECAPA, 128 ResNet, 64 HuBERT)")
+    ap.add_argument("--arch", default="ECAPA_TDNN_c1024",
+                    help=f"ECAPA_TDNN_*, ResNet*, or {HUBERT_ARCH} (wav -> HuBERT -> CMN -> ECAPA)")
     ap.add_argument("--seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -94,6 +105,34 @@ def cpu_baseline(arch: str, sd, num_samples: int, budget_s: float):
                       f"numpy-f64 fbank + torch-CPU fp32 {arch} (oracle restatement), {el:.1f}s"}
 
 
+def cpu_baseline_hubert(sd_fe, sd, num_samples: int, budget_s: float):
+    """Oracle ('port') C4 chain on the host cores: fp32 torch-CPU HuBERT-base +
+    s3prl glue + CMN + ECAPA_TDNN_GLOB_c512.  Bounded sample: batches of 2."""
+    from oracle import hubert_ref, models_ref
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sdf = {k: torch.from_numpy(v) for k, v in sd_fe.items()}
+    sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
+
+    def run(n, seed):
+        wav = torch.from_numpy(synth_audio(seed, n, num_samples, int16_scale=False))
+        with torch.no_grad():
+            f = hubert_ref.s3prl_frontend(wav, sdf)
+            models_ref.forward("ECAPA_TDNN_GLOB_c512", f - f.mean(dim=1, keepdim=True), sdt)
+
+    run(1, 1000)  # warm-up
+    done, t0 = 0, time.perf_counter()
+    while True:
+        run(2, 1001 + done)
+        done += 2
+        el = time.perf_counter() - t0
+        if el >= budget_s or done >= 64:
+            break
+    return {"value": done / el, "unit": "emb/s", "cores": threads, "kind": "port",
+            "sample": f"{done} synthetic {num_samples / 16000:.0f}s utts, batches of 2, torch-CPU fp32 "
+                      f"HuBERT-base + s3prl glue + CMN + ECAPA_TDNN_GLOB_c512 (oracle restatement), {el:.1f}s"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -106,26 +145,40 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    B = args.batch
+    hubert = args.arch == HUBERT_ARCH
+    B = args.batch or (64 if hubert else 128 if args.arch.startswith("ResNet") else 256)
     N = int(round(args.seconds * 16000))
-    emb_dim = 192 if args.arch.startswith("ECAPA") else 256
-    spec = make_spec(args.arch, feat_dim=80, embed_dim=emb_dim)
-    model = HipSpeakerModel(args.arch, feat_dim=80, embed_dim=emb_dim)
+    emb_dim = 256 if args.arch.startswith("ResNet") else 192
+    head_arch = "ECAPA_TDNN_GLOB_c512" if hubert else args.arch
+    feat_dim = 768 if hubert else 80
+    spec = make_spec(head_arch, feat_dim=feat_dim, embed_dim=emb_dim)
+    model = HipSpeakerModel(head_arch, feat_dim=feat_dim, embed_dim=emb_dim)
     sd = synth_state_dict(1234, model.state_dict_layout(), residual_tame=args.arch.startswith("ResNet"))
     model.load_state_dict(sd)
-    model.set_option("precision", args.precision)
-    if args.x3_variant is not None:
-        model.set_option("x3_variant", args.x3_variant)
-    model.to(dev)
+    fe, sd_fe = None, None
+    if hubert:
+        fe = S3prlFrontend({"name": "hubert_base"})
+        sd_fe = synth_state_dict(1235, fe.state_dict_layout())
+        fe.load_state_dict(sd_fe)
+    for mm in (model, fe):
+        if mm is None:
+            continue
+        mm.set_option("precision", args.precision)
+        if args.x3_variant is not None:
+            mm.set_option("x3_variant", args.x3_variant)
+        mm.to(dev)
 
     # inputs resident in HBM before the timed region (per-rank shard)
-    wav = torch.from_numpy(synth_audio(7 + rank, B, N)).to(dev)
-    T = 1 + (N - 400) // 160
-    feats = torch.empty(B, T, 80, device=dev)
+    wav = torch.from_numpy(synth_audio(7 + rank, B, N, int16_scale=not hubert)).to(dev)
+    T = (N + 319) // 320 if hubert else 1 + (N - 400) // 160
+    feats = torch.empty(B, T, feat_dim, device=dev)
     emb = torch.empty(B, emb_dim, device=dev)
 
     def step():
-        compute_fbank(wav, scale=1.0, cmn=True, out=feats)
+        if hubert:
+            fe.extract(wav, cmn=True, out=feats)
+        else:
+            compute_fbank(wav, scale=1.0, cmn=True, out=feats)
         model.embed(feats, out=emb)
 
     def barrier():
@@ -142,6 +195,8 @@ def main():
     # roofline figure below.
     if not args.no_profile:
         model.profile(True)
+        if fe is not None:
+            fe.profile(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -149,6 +204,8 @@ def main():
     el = time.perf_counter() - t0
     if not args.no_profile:
         model.profile(False)
+        if fe is not None:
+            fe.profile(False)
     if dist is not None:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -157,16 +214,33 @@ def main():
 
     kernels, roof = {}, None
     if not args.no_profile:
-        for tag in ("layer1", "conv1x1_CxC", "res2_k3", "se", "conv_cat", "glob_ctx", "pool_linear1",
-                    "pool_linear2", "astp", "head", "stem", "shortcut", "res_conv1x1", "res_conv3x3", "tstp_head"):
-            n, ms, fl = model.profile_query(tag)
+        queries = [(model, t) for t in HEAD_TAGS] + ([(fe, t) for t in HUBERT_TAGS] if fe is not None else [])
+        for mm, tag in queries:
+            n, ms, fl = mm.profile_query(tag)
             if n:
                 avg = ms / n
                 kernels[tag] = {"launches_per_step": n // args.steps, "avg_ms": round(avg, 4),
                                 "ms_per_step": round(ms / args.steps, 4),
                                 "tflops": round(fl / (avg * 1e-3) / 1e12, 2) if fl else None}
-        k = kernels.get("conv1x1_CxC")
-        if k:
+        k = kernels.get("h_fc1") if hubert else kernels.get("conv1x1_CxC")
+        if k and hubert:
+            Th = (N - 400) // 320 + 1  # HuBERT conv frames (249 for 5 s)
+            M, Nn, K = B * Th, 3072, 768
+            flops = 2.0 * M * Nn * K
+            ach = flops / (k["avg_ms"] * 1e-3) / 1e12
+            x3 = args.precision == 1
+            peak = BF16_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+            sym = DOMINANT_GEMM[args.precision]
+            grid = ((M + 255) // 256) * (Nn // 128) * 512 if x3 else ((M + 127) // 128) * (Nn // 128) * 256
+            traffic, src = profiled_traffic(sym, grid)
+            roof = {"kernel": sym + " (HuBERT FFN fc1 + GELU)", "bound": "mfma", "achieved": round(ach, 2),
+                    "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
+                    "traffic_source": src, "algorithmic_bytes": 4.0 * M * (K + Nn) + (4 if x3 else 4) * Nn * K,
+                    "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"],
+                    "mfma_dtype": "bf16 (3-term split, fp32 accumulate)" if x3 else "f32",
+                    "mfma_work_factor": 3 if x3 else 1,
+                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4)}
+        elif k:
             C = 1024 if "c1024" in args.arch else 512
             M = B * T
             flops = 2.0 * M * C * C          # algorithmic: 2*M*N*K, M = B*T frames
@@ -185,7 +259,8 @@ def main():
                     "mfma_work_factor": 3 if x3 else 1,
                     "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4)}
 
-    gf = ecapa_gflop_per_utt(spec, T) if args.arch.startswith("ECAPA") else sum(
+    gf = hubert_gflop_per_utt(N) + ecapa_gflop_per_utt(spec, T) if hubert else ecapa_gflop_per_utt(spec, T) \
+        if args.arch.startswith("ECAPA") else sum(
         v["ms_per_step"] * (v["tflops"] or 0) for v in kernels.values()) / B if kernels else 0.0
     res = {
         "metric": "embeddings/sec on 5s 16kHz utts",
@@ -199,8 +274,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (clip(N(0,0.1)) x32768 PCM16-valued audio, seeded random-init weights)",
-        "config": {"workload": f"{args.arch} fbank80 extract, {args.seconds:g}s 16kHz utts",
+        "data": ("synthetic (clip(N(0,0.1)) [-1,1] audio, seeded random-init weights)" if hubert else
+                 "synthetic (clip(N(0,0.1)) x32768 PCM16-valued audio, seeded random-init weights)"),
+        "config": {"workload": (f"HuBERT-base (s3prl featurizer) + CMN + ECAPA_TDNN_GLOB_c512 extract, "
+                                f"{args.seconds:g}s 16kHz utts" if hubert else
+                                f"{args.arch} fbank80 extract, {args.seconds:g}s 16kHz utts"),
                    "arch": args.arch, "batch_per_gpu": B, "global_batch": B * world,
                    "samples_per_utt": N, "frames": T, "parallelism": f"dp{world}"},
         "model_tflops": round(value * gf / 1e3, 2),
@@ -210,7 +288,8 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(args.arch, sd, N, args.cpu_seconds)
+        res["cpu_baseline"] = (cpu_baseline_hubert(sd_fe, sd, N, args.cpu_seconds) if hubert else
+                               cpu_baseline(args.arch, sd, N, args.cpu_seconds))
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:

@@ -79,7 +79,9 @@ int wsp_fbank(const void* wav, int wav_dtype, int B, int num_samples, int ld, fl
 
 /* ------------------------------------------------------------- model --- */
 /* arch: "ECAPA_TDNN_c512", "ECAPA_TDNN_GLOB_c512", "ECAPA_TDNN_c1024",
- * "ECAPA_TDNN_GLOB_c1024", "ResNet18/34/50/101/152/221/293" */
+ * "ECAPA_TDNN_GLOB_c1024", "ResNet18/34/50/101/152/221/293"
+ * (wespeaker/models/speaker_model.py:30-57), or the SSL front end
+ * "HuBERT_base" (embed_dim 768; wespeaker/frontend/s3prl.py:23-75). */
 int wsp_model_create(const char* arch, int feat_dim, int embed_dim, int emb_bn,
                      int two_emb_layer, wsp_model** out);
 int wsp_model_destroy(wsp_model* m);
@@ -103,7 +105,10 @@ int wsp_model_forward(wsp_model* m, const float* feats, int B, int T, float* emb
 /* Runtime options (any time after create):
  *   "precision"  1 = bf16x3 split MFMA (default; fp32-class accuracy),
  *                0 = exact f32 MFMA
- *   "x3_variant" bf16x3 block tile: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves) */
+ *   "x3_variant" bf16x3 block tile: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves),
+ *                2 = LDS-DMA staged 256x128 where supported
+ *   "layer"      HuBERT front end only, before finalize: -1 = weighted sum of all
+ *                hidden states (default), k = hidden state k alone (s3prl.py:84-87) */
 int wsp_model_set_option(wsp_model* m, const char* key, int value);
 
 /* Per-kernel-class timing with HIP events recorded on the launch stream
@@ -113,6 +118,22 @@ int wsp_model_profile(wsp_model* m, int enable);
  * FLOPs per launch of the named kernel class, then clears it. */
 int wsp_model_profile_query(wsp_model* m, const char* kernel_class, int* launches,
                             double* total_ms, double* flops_per_launch);
+
+/* ----------------------------------------------- SSL front end (HuBERT) --- */
+/* Replaces S3prlFrontend.forward (wespeaker/frontend/s3prl.py:80-93): s3prl
+ * HuBERT-base upstream -> Featurizer (softmax-weighted sum of the 13 hidden
+ * states, or the single state chosen with wsp_model_set_option(m, "layer", k)
+ * before finalize) -> s3prl length match, optionally followed by
+ * bin/extract.py:104-106's apply_cmvn (cmn = 1).  Handles come from
+ * wsp_model_create("HuBERT_base", 1, 768, 0, 0, &m); parameters are the
+ * reference checkpoint's "frontend.*" entries. */
+/* Frames per utterance: len(range(0, num_samples, 320)). num_samples >= 400. */
+int wsp_frontend_out_frames(const wsp_model* m, int num_samples, int* frames);
+int wsp_frontend_workspace_bytes(const wsp_model* m, int B, int num_samples, size_t* bytes);
+/* wav [B][num_samples] f32 in [-1, 1] (bin/extract.py:100-102: not x32768)
+ * -> feats [B][frames][768] f32.  Asynchronous on `stream`. */
+int wsp_frontend_forward(wsp_model* m, const float* wav, int B, int num_samples, float* feats, int cmn,
+                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------ scoring --- */
 /* y[r] = x[r] - sub (sub may be NULL), then L2-normalised; [R][D] f32. */

@@ -1,0 +1,126 @@
+"""GPU parity of the HuBERT-base SSL front end and
+the C4 chain HuBERT -> CMN -> ECAPA_TDNN_GLOB_c512(feat_dim 768).
+
+Checker: oracle/hubert_ref.py (fp32 torch-CPU restatement, pinned against the
+transformers HubertModel proxy fixture tests/golden/hubert_proxy.npz; the s3prl
+glue itself is parity-unpinned — s3prl is absent offline).
+Tolerances: hidden states / features |delta| <= 2e-4 (LayerNorm-scaled O(1)
+values after 12 fp32-class layers); embeddings per-dim |delta| < 1e-4 and
+cosine >= 0.9999 (BASELINE.json north_star).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import hubert_ref, models_ref  # noqa: E402
+from wespeaker_hubert_amd.arch import hubert_params, s3prl_num_frames  # noqa: E402
+from wespeaker_hubert_amd.synthetic import synth_audio, synth_state_dict  # noqa: E402
+
+DEV = "cuda:0"
+FEAT_ATOL = 2e-4
+EMB_ATOL = 1e-4
+EMB_COS = 0.9999
+SEED = 41
+
+
+@pytest.fixture(scope="module")
+def sd_np():
+    return synth_state_dict(SEED, hubert_params())
+
+
+@pytest.fixture(scope="module")
+def sd_t(sd_np):
+    return {k: torch.from_numpy(v) for k, v in sd_np.items()}
+
+
+def _frontend(sd_np, layer=-1, precision=1, multilayer=True):
+    from wespeaker_hubert_amd.s3prl_frontend import S3prlFrontend
+    fe = S3prlFrontend({"name": "hubert_base"}, multilayer_feature=multilayer, layer=layer)
+    fe.set_option("precision", precision)
+    fe.load_state_dict(sd_np)
+    return fe.to(DEV)
+
+
+def _wav(seed, B, W):
+    return synth_audio(seed, B, W, int16_scale=False)
+
+
+def _cmn(x):
+    return x - x.mean(dim=1, keepdim=True)
+
+
+@pytest.mark.parametrize("layer", [0, 1, 6, 12])
+def test_hidden_state_matches_oracle(sd_np, sd_t, layer):
+    wav = _wav(7, 2, 16000)
+    fe = _frontend(sd_np, layer=layer, multilayer=False)
+    got = fe.extract(torch.from_numpy(wav).to(DEV)).cpu()
+    with torch.no_grad():
+        hs = hubert_ref.hubert_hidden_states(torch.from_numpy(wav), sd_t)
+    ref = hubert_ref.match_length(hs[layer], wav.shape[1])
+    assert got.shape == ref.shape == (2, 50, 768)
+    d = (got - ref).abs().max().item()
+    assert d <= FEAT_ATOL, f"layer {layer}: max |delta| {d}"
+
+
+@pytest.mark.parametrize("precision", [1, 0], ids=["bf16x3", "f32"])
+@pytest.mark.parametrize("W", [16000, 12345, 400])
+def test_featurizer_output_matches_oracle(sd_np, sd_t, precision, W):
+    wav = _wav(8, 2, W)
+    fe = _frontend(sd_np, precision=precision)
+    x = torch.from_numpy(wav).to(DEV)
+    got = fe.extract(x).cpu()
+    got_cmn = fe.extract(x, cmn=True).cpu()
+    with torch.no_grad():
+        ref = hubert_ref.s3prl_frontend(torch.from_numpy(wav), sd_t)
+    assert got.shape == ref.shape == (2, s3prl_num_frames(W), 768)
+    assert (got - ref).abs().max().item() <= FEAT_ATOL
+    assert (got_cmn - _cmn(ref)).abs().max().item() <= FEAT_ATOL
+    feats, lens = fe(x, torch.full((2,), W, dtype=torch.long))
+    assert torch.equal(feats.cpu(), got) and lens.tolist() == [s3prl_num_frames(W)] * 2
+
+
+def test_last_layer_when_not_multilayer(sd_np, sd_t):
+    """multilayer_feature=False, layer=-1: featurizer over feats[-1:] (s3prl.py:88-91)."""
+    wav = _wav(9, 1, 8000)
+    got = _frontend(sd_np, multilayer=False).extract(torch.from_numpy(wav).to(DEV)).cpu()
+    with torch.no_grad():
+        ref = hubert_ref.match_length(hubert_ref.hubert_hidden_states(torch.from_numpy(wav), sd_t)[-1], 8000)
+    assert (got - ref).abs().max().item() <= FEAT_ATOL
+
+
+def test_batch_rows_independent_and_chunked(sd_np):
+    """Size-independent property at the bench shape: a 5 s batch big enough to
+    split the feature extractor into utterance chunks gives every row exactly
+    what a batch of one gives."""
+    B, W = 60, 80000
+    wav = torch.from_numpy(_wav(10, B, W)).to(DEV)
+    fe = _frontend(sd_np)
+    full = fe.extract(wav, cmn=True)
+    for i in (0, 31, B - 1):
+        one = fe.extract(wav[i:i + 1].contiguous(), cmn=True)
+        d = (full[i] - one[0]).abs().max().item()
+        assert d <= 1e-5, f"row {i}: {d}"
+    assert torch.isfinite(full).all()
+
+
+def test_hubert_ecapa_chain_embeddings(sd_np, sd_t):
+    """C4: wav -> HuBERT -> CMN -> ECAPA_TDNN_GLOB_c512(feat_dim=768) -> embed."""
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    wav = _wav(11, 3, 24000)
+    fe = _frontend(sd_np)
+    m = HipSpeakerModel("ECAPA_TDNN_GLOB_c512", feat_dim=768, embed_dim=192)
+    sd_e = synth_state_dict(12, m.state_dict_layout())
+    m.load_state_dict(sd_e)
+    m.to(DEV)
+    feats = fe.extract(torch.from_numpy(wav).to(DEV), cmn=True)
+    got = m(feats)[-1].cpu().numpy()
+    with torch.no_grad():
+        f_ref = _cmn(hubert_ref.s3prl_frontend(torch.from_numpy(wav), sd_t))
+        ref = models_ref.forward("ECAPA_TDNN_GLOB_c512", f_ref,
+                                 {k: torch.from_numpy(v) for k, v in sd_e.items()})[-1].numpy()
+    d = np.abs(got - ref).max()
+    cos = (got * ref).sum(1) / (np.linalg.norm(got, axis=1) * np.linalg.norm(ref, axis=1))
+    assert d < EMB_ATOL, f"max |delta| {d}"
+    assert cos.min() >= EMB_COS

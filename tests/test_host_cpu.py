@@ -40,3 +40,25 @@ def test_cpu_device_is_refused():
 def test_flop_count_c1024():
     spec = A.make_spec("ECAPA_TDNN_c1024", feat_dim=80, embed_dim=192)
     assert abs(A.ecapa_gflop_per_utt(spec, 498) - 12.80) < 0.05
+
+
+def test_s3prl_frontend_intake_and_options(caplog):
+    """S3prlFrontend mirror (frontend/s3prl.py:23-93): reference checkpoint names with
+    or without the `frontend.` prefix, fairseq-only members ignored silently."""
+    from wespeaker_hubert_amd.s3prl_frontend import S3prlFrontend
+    fe = S3prlFrontend({"name": "hubert_base"})
+    assert fe.output_size() == 768 and fe._options["layer"] == -1
+    lay = fe.state_dict_layout()
+    sd = {k[len("frontend."):]: np.zeros(s, np.float32) for k, s in lay[:3]}
+    sd["upstream.upstream.model.mask_emb"] = np.zeros(768, np.float32)
+    sd["upstream.upstream.model.final_proj.weight"] = np.zeros((256, 768), np.float32)
+    missing, unexpected = fe.load_state_dict(sd)
+    assert unexpected == [] and len(missing) == len(lay) - 3
+    assert S3prlFrontend({"name": "hubert_base"}, multilayer_feature=False)._options["layer"] == 12
+    assert S3prlFrontend({"name": "hubert"}, multilayer_feature=False, layer=4)._options["layer"] == 4
+    with pytest.raises(AssertionError):
+        S3prlFrontend({"name": "hubert_base"}, layer=3)
+    with pytest.raises(NotImplementedError):
+        S3prlFrontend({"name": "wavlm_large"})
+    with pytest.raises(RuntimeError):
+        fe.to("cpu")

@@ -36,6 +36,10 @@ SIGNATURES = {
     "wsp_model_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_size_t,
                                   c_void_p]),
     "wsp_model_set_option": (c_int, [c_void_p, c_char_p, c_int]),
+    "wsp_frontend_out_frames": (c_int, [c_void_p, c_int, POINTER(c_int)]),
+    "wsp_frontend_workspace_bytes": (c_int, [c_void_p, c_int, c_int, POINTER(c_size_t)]),
+    "wsp_frontend_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_size_t,
+                                     c_void_p]),
     "wsp_model_profile": (c_int, [c_void_p, c_int]),
     "wsp_model_profile_query": (c_int, [c_void_p, c_char_p, POINTER(c_int), POINTER(c_double),
                                         POINTER(c_double)]),

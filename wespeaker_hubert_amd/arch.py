@@ -203,3 +203,17 @@ def hubert_num_frames(num_samples: int, cfg=HUBERT_BASE) -> int:
 def s3prl_num_frames(num_samples: int, downsample_rate: int = 320) -> int:
     """len(range(0, W, 320)) — s3prl's length match target."""
     return (num_samples + downsample_rate - 1) // downsample_rate
+
+
+def hubert_gflop_per_utt(num_samples: int, cfg=HUBERT_BASE) -> float:
+    """Algorithmic FLOPs (2 x MACs) of the HuBERT-base front end on one utterance."""
+    c, h, L = cfg["conv_dim"], cfg["hidden"], cfg["layers"]
+    t = num_samples
+    macs = 0
+    for i, (k, s) in enumerate(zip(cfg["conv_kernel"], cfg["conv_stride"])):
+        t = (t - k) // s + 1
+        macs += t * c * k * (1 if i == 0 else c)
+    macs += t * c * h                                               # post_extract_proj
+    macs += t * h * (h // cfg["pos_groups"]) * cfg["pos_k"]         # grouped pos_conv
+    per_layer = t * h * 3 * h + 2 * t * t * h + t * h * h + 2 * t * h * cfg["ffn"]
+    return 2.0 * (macs + L * per_layer) / 1e9

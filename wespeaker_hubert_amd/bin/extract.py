@@ -10,12 +10,15 @@ Semantics (bin/extract.py:33-120, dataset/dataset.py:136-247):
     ((num_frms-1)*frame_shift + frame_length)*sr/1000 samples per utterance
     (processor.get_random_chunk, repeat-padded when shorter) — seeded here
     (`--chunk_seed`, default 0) so extraction is reproducible;
-  * fbank on the GPU with dither 0, CMN (apply_cmvn norm_mean) fused;
+  * fbank on the GPU with dither 0, CMN (apply_cmvn norm_mean) fused; or,
+    with `dataset_args.frontend: s3prl` (hubert_base), the HuBERT front end
+    on [-1, 1] audio (extract.py:100-102) + CMN, then the backbone on its
+    768-dim frames;
   * under torchrun (WORLD_SIZE > 1) the data list is split into contiguous
     parts exactly like tools/extract_embedding.sh:40-42 and rank r writes
     `<embed_ark stem>_<r:03d>.ark/.scp` (cat the scps in rank order).
 Audio decode runs on a host thread pool (`--num-workers`); augmentation
-(aug_prob > 0) and the s3prl front end are not available on this path.
+(aug_prob > 0) is not available on this path.
 """
 from __future__ import annotations
 
@@ -38,6 +41,7 @@ from .. import audio
 from ..dist import shard_lines
 from ..frontend import compute_fbank
 from ..kaldi_io import WriteHelper, validate_path
+from ..s3prl_frontend import S3prlFrontend
 from ..speaker_model import get_speaker_model
 from . import _fire
 
@@ -107,8 +111,8 @@ def extract(config="conf/config.yaml", **kwargs):
     num_workers = max(1, int(configs.get("num_workers", 1)))
     test_conf = copy.deepcopy(configs["dataset_args"])
     frontend_type = test_conf.get("frontend", "fbank")
-    if frontend_type != "fbank":
-        raise NotImplementedError(f"frontend {frontend_type!r} is not available on the MI355X path yet")
+    if frontend_type not in ("fbank", "s3prl"):
+        raise NotImplementedError(f"frontend {frontend_type!r} is not available on the MI355X path")
     if float(configs.get("aug_prob", 0.0) or 0.0) > 0:
         logging.warning("aug_prob > 0 ignored: augmentation is out of scope at extraction")
     cmvn_args = test_conf.get("cmvn_args", {}) or {}
@@ -116,11 +120,16 @@ def extract(config="conf/config.yaml", **kwargs):
         raise NotImplementedError("only apply_cmvn(norm_mean=True, norm_var=False) is implemented")
     if not test_conf.get("cmvn", True):
         raise NotImplementedError("cmvn=False is not implemented")
-    fb = test_conf.get("fbank_args", {})
-    if int(fb.get("num_mel_bins", 80)) != 80 or int(fb.get("frame_shift", 10)) != 10 \
-            or int(fb.get("frame_length", 25)) != 25:
-        raise NotImplementedError("fbank implemented for 80 bins, 25/10 ms")
     sr_target = int(test_conf.get("resample_rate", 16000))
+    if frontend_type == "fbank":
+        fb = test_conf.get("fbank_args", {})
+        if int(fb.get("num_mel_bins", 80)) != 80 or int(fb.get("frame_shift", 10)) != 10 \
+                or int(fb.get("frame_length", 25)) != 25:
+            raise NotImplementedError("fbank implemented for 80 bins, 25/10 ms")
+        frame_shift, frame_length = 10, 25
+    else:
+        fa = test_conf["s3prl_args"]
+        frame_shift, frame_length = int(fa.get("frame_shift", 10)), int(fa.get("frame_length", 25))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -129,8 +138,19 @@ def extract(config="conf/config.yaml", **kwargs):
         torch.cuda.set_device(local % torch.cuda.device_count())
     device = torch.device("cuda", torch.cuda.current_device())
 
-    model = get_speaker_model(configs["model"])(**configs["model_args"])
+    model_args = dict(configs["model_args"])
+    frontend = None
+    if frontend_type == "s3prl":
+        # extract.py:49-55: model.add_module("frontend", frontend_class(**s3prl_args, sample_rate=...))
+        frontend = S3prlFrontend(**test_conf["s3prl_args"], sample_rate=sr_target)
+        if int(model_args.get("feat_dim", -1)) == -1:  # bin/train.py:117-119
+            model_args["feat_dim"] = frontend.output_size()
+    model = get_speaker_model(configs["model"])(**model_args)
     state = torch.load(model_path, map_location="cpu", weights_only=True)
+    if frontend is not None:
+        frontend.load_state_dict({k: v for k, v in state.items() if k.startswith("frontend.")})
+        state = {k: v for k, v in state.items() if not k.startswith("frontend.")}
+        frontend.to(device)
     model.load_state_dict(state, strict=False)
     model.to(device)
 
@@ -154,11 +174,14 @@ def extract(config="conf/config.yaml", **kwargs):
 
     rng = random.Random(int(configs.get("chunk_seed", 0)))
     num_frms = int(test_conf.get("num_frms", 200))
-    chunk_len = ((num_frms - 1) * 10 + 25) * sr_target // 1000
+    chunk_len = ((num_frms - 1) * frame_shift + frame_length) * sr_target // 1000  # dataset.py:212-215
 
     def run(keys, wavs, writer):
         x = torch.from_numpy(np.stack(wavs).astype(np.float32)).to(device)
-        feats = compute_fbank(x, scale=1.0, cmn=True)
+        if frontend is None:
+            feats = compute_fbank(x, scale=1.0, cmn=True)
+        else:  # torchaudio.load(normalize=True) audio in [-1, 1]; apply_cmvn fused
+            feats = frontend.extract(x * (1.0 / 32768.0), cmn=True)
         emb = model(feats)[-1].cpu().numpy()
         for k, e in zip(keys, emb):
             writer(k, e)

@@ -147,6 +147,28 @@ int wsp_model_forward(wsp_model* m, const float* feats, int B, int T, float* emb
   });
 }
 
+int wsp_frontend_out_frames(const wsp_model* m, int num_samples, int* frames) {
+  WSP_GUARD({
+    WSP_CHECK(m && frames, "null argument");
+    *frames = m->m.out_frames(num_samples);
+  });
+}
+
+int wsp_frontend_workspace_bytes(const wsp_model* m, int B, int num_samples, size_t* bytes) {
+  WSP_GUARD({
+    WSP_CHECK(m && bytes, "null argument");
+    *bytes = m->m.frontend_workspace_bytes(B, num_samples);
+  });
+}
+
+int wsp_frontend_forward(wsp_model* m, const float* wav, int B, int num_samples, float* feats, int cmn,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(m && wav && feats && workspace, "null argument");
+    m->m.forward_frontend(wav, B, num_samples, feats, cmn, workspace, workspace_bytes, S(stream));
+  });
+}
+
 int wsp_model_set_option(wsp_model* m, const char* key, int value) {
   WSP_GUARD({
     WSP_CHECK(m && key, "null argument");

@@ -115,6 +115,34 @@ void fbank_tables(float* host_tab);  // window, twiddles, sparse mel filters
 void launch_fbank(const void* wav, int dtype, int B, int N, int ld, float scale, float* feats,
                   int T, int cmn, const float* tables, hipStream_t s);
 
+// HuBERT-base front end (hubert.hip).
+// conv0 (1 -> 512, k10 s5, no bias) + GroupNorm(512, 512) + GELU:
+// wav [B][ldw] (N samples) -> out [B][T0][512]; stats = [2][B][512] doubles scratch.
+void launch_hubert_conv0(const float* wav, int B, int N, int ldw, int T0, const float* w, const float* gamma,
+                         const float* beta, double* stats, float* out, hipStream_t s);
+// out[row] = LayerNorm(x[row] (+ add[row][remap(c)])) with remap(c) = (c/gin)*gout + c%gin;
+// if feat: feat[b][t'] (=|+=) feat_w * out[row] for t' = t, and t' in [T, Tout) when t = T-1.
+struct LayerNormArgs {
+  const float* x;
+  int ldx;
+  const float* add;
+  int ldadd, gin, gout;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  float* out;
+  int ldo;
+  int M, D;
+  float* feat;
+  float feat_w;
+  int feat_init, T, Tout;
+};
+void launch_layernorm(const LayerNormArgs& p, hipStream_t s);
+// softmax(Q K^T / sqrt(dh)) V per (utterance, head); qkv [B*T][ldq] = [q | k | v] (H*dh each).
+void launch_mha(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s);
+// x [B][T][D] -= mean over T  (apply_cmvn(norm_mean=True, norm_var=False))
+void launch_cmn_rows(float* x, int B, int T, int D, hipStream_t s);
+
 // Scoring helpers.
 void launch_l2_normalize(const float* x, const float* sub, float* y, int R, int D, hipStream_t s);
 void launch_cosine_pairs(const float* E, int D, const int32_t* ia, const int32_t* ib, int P,

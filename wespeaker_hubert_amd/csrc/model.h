@@ -22,6 +22,12 @@ class Model {
   size_t workspace_bytes(int B, int T) const;
   void forward(const float* feats, int B, int T, float* embed, void* ws, size_t ws_bytes,
                hipStream_t s);
+  // HuBERT front end (arch "HuBERT_base"): wav [B][N] -> feats [B][out_frames(N)][768]
+  bool is_frontend() const;
+  int out_frames(int N) const;
+  size_t frontend_workspace_bytes(int B, int N) const;
+  void forward_frontend(const float* wav, int B, int N, float* feats, int cmn, void* ws, size_t ws_bytes,
+                        hipStream_t s);
   void profile(bool on);
   void set_option(const std::string& key, int value);
   void profile_query(const std::string& tag, int* launches, double* total_ms, double* flops);

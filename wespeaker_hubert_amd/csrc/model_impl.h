@@ -1,0 +1,739 @@
+// Internal: the Model::Impl runtime object shared by the ECAPA / ResNet
+// (model.cpp) and HuBERT (hubert_model.cpp) translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "model.h"
+
+namespace wsp {
+
+namespace detail {
+
+constexpr double kBnEps = 1e-5;
+
+struct DevBuf {
+  std::vector<void*> ptrs;
+  ~DevBuf() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  void* upload_u16(const std::vector<uint16_t>& v) {
+    void* p = nullptr;
+    WSP_HIP(hipMalloc(&p, std::max<size_t>(v.size(), 1) * sizeof(uint16_t)));
+    ptrs.push_back(p);
+    if (!v.empty()) WSP_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    return p;
+  }
+  float* upload(const std::vector<float>& v) {
+    void* p = nullptr;
+    WSP_HIP(hipMalloc(&p, std::max<size_t>(v.size(), 1) * sizeof(float)));
+    ptrs.push_back(p);
+    if (!v.empty()) WSP_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice));
+    return static_cast<float*>(p);
+  }
+};
+
+struct ConvW {
+  float* w = nullptr;
+  void* whi = nullptr;  // bf16 hi / lo split images for the bf16x3 kernel
+  void* wlo = nullptr;
+  float* bias = nullptr;
+  float* scale = nullptr;
+  float* shift = nullptr;
+  int N = 0, cin = 0, taps = 1, K = 0, Kp = 0;
+};
+
+struct LinW {  // small_linear weights, k-major
+  float* wt = nullptr;
+  float* bias = nullptr;
+  int K = 0, N = 0;
+};
+
+inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+// fp32 -> bf16, round to nearest even (matches v_cvt_pk_bf16_f32 on finite values)
+inline uint16_t f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+inline float bf2f(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+}  // namespace detail
+
+using namespace detail;
+
+struct Param {
+  std::string name;
+  std::vector<int64_t> shape;
+  std::vector<float> host;
+  bool set = false;
+  int64_t numel() const {
+    int64_t n = 1;
+    for (auto s : shape) n *= s;
+    return n;
+  }
+};
+
+struct ProfEntry {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t used = 0;
+  double flops = 0;
+};
+
+struct Model::Impl {
+  std::string arch;
+  bool ecapa = true;
+  int C = 512;
+  bool glob = false;
+  int feat_dim = 80, embed_dim = 192;
+  bool emb_bn = false, two_emb = false;
+  std::vector<Param> params;
+  std::map<std::string, int> idx;
+  bool finalized = false;
+  int device = 0;
+  DevBuf dev;
+
+  // ECAPA packed weights
+  ConvW layer1;
+  struct Block {
+    ConvW c1, c3, res2[7];
+    LinW se1, se2;
+  } blk[3];
+  ConvW conv, pool1, pool2;
+  LinW pool1_ctx;
+  LinW head;
+
+  // ResNet (resnet.py:110-260), NHWC activations [B][F][T][C]
+  bool bottleneck = true;
+  int nblocks[4] = {0, 0, 0, 0};
+  int m_ch = 32;
+  float* stem_w = nullptr;
+  float* stem_b = nullptr;
+  struct RBlock {
+    ConvW c1, c2, c3, sc;
+    bool has_sc = false;
+    int stride = 1, in_planes = 0, planes = 0, out_planes = 0;
+  };
+  std::vector<RBlock> rblocks;
+  LinW seg1;
+
+  // HuBERT-base front end (hubert_model.cpp), channels-last [B][T][C]
+  bool hubert = false;
+  float* h_conv0_w = nullptr;  // [512][10]
+  float* h_gn_g = nullptr;
+  float* h_gn_b = nullptr;
+  ConvW h_conv[7];  // 1..6: strided feature-extractor convs (GELU epilogue)
+  float* h_ln0_g = nullptr;
+  float* h_ln0_b = nullptr;
+  ConvW h_proj, h_pos;
+  float* h_enc_g = nullptr;
+  float* h_enc_b = nullptr;
+  struct HLayer {
+    ConvW qkv, out, fc1, fc2;
+    float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
+  };
+  std::vector<HLayer> h_layers;
+  std::vector<float> h_fw;  // featurizer weight per hidden state
+  int h_layer_sel = -1;     // s3prl `layer` (-1: softmax-weighted sum of all 13)
+  void build_hubert_params();
+  void finalize_hubert();
+  int hubert_cnn_frames(int N, int upto) const;
+  int hubert_chunk(int B, int N) const;
+  size_t hubert_ws_floats(int B, int N, size_t* offs) const;
+  void forward_hubert(const float* wav, int B, int N, float* feats, int cmn, float* ws, hipStream_t s);
+
+  // 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA
+  int precision = 1;
+  int x3_variant = 1;
+
+  // profiling
+  bool prof = false;
+  std::map<std::string, ProfEntry> prof_map;
+
+  void add(const std::string& n, std::vector<int64_t> shape) {
+    idx[n] = (int)params.size();
+    params.push_back(Param{n, std::move(shape), {}, false});
+  }
+  void add_bn(const std::string& p, int64_t c) {
+    add(p + ".weight", {c});
+    add(p + ".bias", {c});
+    add(p + ".running_mean", {c});
+    add(p + ".running_var", {c});
+    add(p + ".num_batches_tracked", {});
+  }
+  const std::vector<float>& P(const std::string& n) const {
+    auto it = idx.find(n);
+    WSP_CHECK(it != idx.end(), "missing parameter " + n);
+    const Param& p = params[it->second];
+    WSP_CHECK(p.set || p.numel() == 0, "parameter not set: " + n);
+    return p.host;
+  }
+
+  // eval BatchNorm as affine: y = x*scale + shift
+  void bn_affine(const std::string& p, std::vector<double>& sc, std::vector<double>& sh) const {
+    const auto& w = P(p + ".weight");
+    const auto& b = P(p + ".bias");
+    const auto& rm = P(p + ".running_mean");
+    const auto& rv = P(p + ".running_var");
+    sc.resize(w.size());
+    sh.resize(w.size());
+    for (size_t i = 0; i < w.size(); ++i) {
+      sc[i] = (double)w[i] / std::sqrt((double)rv[i] + kBnEps);
+      sh[i] = (double)b[i] - (double)rm[i] * sc[i];
+    }
+  }
+
+  // Conv1d weight [N][cin][taps] -> packed [N][Kp], k = tap*cin + c.
+  ConvW pack_conv(const std::vector<float>& w, int N, int cin, int taps, const float* bias,
+                  const std::string& bn) {
+    ConvW cw;
+    cw.N = N;
+    cw.cin = cin;
+    cw.taps = taps;
+    cw.K = cin * taps;
+    cw.Kp = round_up(cw.K, 64);  // even number of 32-wide k-tiles (bf16x3 pipeline)
+    std::vector<float> packed((size_t)N * cw.Kp, 0.f);
+    for (int n = 0; n < N; ++n)
+      for (int c = 0; c < cin; ++c)
+        for (int j = 0; j < taps; ++j)
+          packed[(size_t)n * cw.Kp + j * cin + c] = w[((size_t)n * cin + c) * taps + j];
+    cw.w = dev.upload(packed);
+    {
+      std::vector<uint16_t> hi(packed.size()), lo(packed.size());
+      for (size_t i = 0; i < packed.size(); ++i) {
+        hi[i] = f2bf(packed[i]);
+        lo[i] = f2bf(packed[i] - bf2f(hi[i]));
+      }
+      cw.whi = dev.upload_u16(hi);
+      cw.wlo = dev.upload_u16(lo);
+    }
+    if (bias) cw.bias = dev.upload(std::vector<float>(bias, bias + N));
+    if (!bn.empty()) {
+      std::vector<double> sc, sh;
+      bn_affine(bn, sc, sh);
+      std::vector<float> s(N), t(N);
+      for (int i = 0; i < N; ++i) {
+        s[i] = (float)sc[i];
+        t[i] = (float)sh[i];
+      }
+      cw.scale = dev.upload(s);
+      cw.shift = dev.upload(t);
+    }
+    return cw;
+  }
+
+  // Linear weight [N][K] (row-major, ldk) -> k-major [K][N]
+  LinW pack_lin(const float* w, int N, int K, int ldk, const float* bias) {
+    LinW lw;
+    lw.N = N;
+    lw.K = K;
+    std::vector<float> t((size_t)K * N);
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < K; ++k) t[(size_t)k * N + n] = w[(size_t)n * ldk + k];
+    lw.wt = dev.upload(t);
+    if (bias) lw.bias = dev.upload(std::vector<float>(bias, bias + N));
+    return lw;
+  }
+
+  void build_ecapa_params() {
+    const int64_t C = this->C, w = C / 8;
+    add("layer1.conv.weight", {C, feat_dim, 5});
+    add("layer1.conv.bias", {C});
+    add_bn("layer1.bn", C);
+    for (int li = 2; li <= 4; ++li) {
+      const std::string p = "layer" + std::to_string(li) + ".se_res2block";
+      add(p + ".0.conv.weight", {C, C, 1});
+      add(p + ".0.conv.bias", {C});
+      add_bn(p + ".0.bn", C);
+      for (int i = 0; i < 7; ++i) {
+        add(p + ".1.convs." + std::to_string(i) + ".weight", {w, w, 3});
+        add(p + ".1.convs." + std::to_string(i) + ".bias", {w});
+      }
+      for (int i = 0; i < 7; ++i) add_bn(p + ".1.bns." + std::to_string(i), w);
+      add(p + ".2.conv.weight", {C, C, 1});
+      add(p + ".2.conv.bias", {C});
+      add_bn(p + ".2.bn", C);
+      add(p + ".3.linear1.weight", {128, C});
+      add(p + ".3.linear1.bias", {128});
+      add(p + ".3.linear2.weight", {C, 128});
+      add(p + ".3.linear2.bias", {C});
+    }
+    add("conv.weight", {1536, 3 * C, 1});
+    add("conv.bias", {1536});
+    add("pool.linear1.weight", {128, glob ? 4608 : 1536, 1});
+    add("pool.linear1.bias", {128});
+    add("pool.linear2.weight", {1536, 128, 1});
+    add("pool.linear2.bias", {1536});
+    add_bn("bn", 3072);
+    add("linear.weight", {embed_dim, 3072});
+    add("linear.bias", {embed_dim});
+    if (emb_bn) add_bn("bn2", embed_dim);
+  }
+
+  void build_resnet_params() {
+    const int exp = bottleneck ? 4 : 1;
+    add("conv1.weight", {m_ch, 1, 3, 3});
+    add_bn("bn1", m_ch);
+    int in_planes = m_ch;
+    for (int li = 0; li < 4; ++li) {
+      const int planes = m_ch << li;
+      for (int bi = 0; bi < nblocks[li]; ++bi) {
+        const int stride = (li > 0 && bi == 0) ? 2 : 1;
+        const std::string p = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+        RBlock rb;
+        rb.stride = stride;
+        rb.in_planes = in_planes;
+        rb.planes = planes;
+        rb.out_planes = planes * exp;
+        if (bottleneck) {
+          add(p + ".conv1.weight", {planes, in_planes, 1, 1});
+          add_bn(p + ".bn1", planes);
+          add(p + ".conv2.weight", {planes, planes, 3, 3});
+          add_bn(p + ".bn2", planes);
+          add(p + ".conv3.weight", {planes * 4, planes, 1, 1});
+          add_bn(p + ".bn3", planes * 4);
+        } else {
+          add(p + ".conv1.weight", {planes, in_planes, 3, 3});
+          add_bn(p + ".bn1", planes);
+          add(p + ".conv2.weight", {planes, planes, 3, 3});
+          add_bn(p + ".bn2", planes);
+        }
+        if (stride != 1 || in_planes != exp * planes) {
+          rb.has_sc = true;
+          add(p + ".shortcut.0.weight", {exp * planes, in_planes, 1, 1});
+          add_bn(p + ".shortcut.1", exp * planes);
+        }
+        rblocks.push_back(rb);
+        in_planes = planes * exp;
+      }
+    }
+    const int stats_dim = (feat_dim / 8) * m_ch * 8 * exp;
+    add("seg_1.weight", {embed_dim, stats_dim * 2});
+    add("seg_1.bias", {embed_dim});
+  }
+
+  // conv -> BN (eval) folded into the weights: W' = W * s[n], bias = shift.
+  ConvW pack_conv_bn(const std::string& wname, const std::string& bn, int N, int cin, int taps) {
+    std::vector<double> sc, sh;
+    bn_affine(bn, sc, sh);
+    std::vector<float> w = P(wname);
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < cin * taps; ++k) w[(size_t)n * cin * taps + k] = (float)(w[(size_t)n * cin * taps + k] * sc[n]);
+    std::vector<float> b(N);
+    for (int n = 0; n < N; ++n) b[n] = (float)sh[n];
+    return pack_conv(w, N, cin, taps, b.data(), "");
+  }
+
+  void finalize_resnet() {
+    {
+      std::vector<double> sc, sh;
+      bn_affine("bn1", sc, sh);
+      const auto& w = P("conv1.weight");
+      std::vector<float> wf(m_ch * 9), bf(m_ch);
+      for (int c = 0; c < m_ch; ++c) {
+        for (int q = 0; q < 9; ++q) wf[c * 9 + q] = (float)(w[c * 9 + q] * sc[c]);
+        bf[c] = (float)sh[c];
+      }
+      stem_w = dev.upload(wf);
+      stem_b = dev.upload(bf);
+    }
+    int idx_b = 0;
+    for (int li = 0; li < 4; ++li)
+      for (int bi = 0; bi < nblocks[li]; ++bi) {
+        RBlock& rb = rblocks[idx_b++];
+        const std::string p = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+        if (bottleneck) {
+          rb.c1 = pack_conv_bn(p + ".conv1.weight", p + ".bn1", rb.planes, rb.in_planes, 1);
+          rb.c2 = pack_conv_bn(p + ".conv2.weight", p + ".bn2", rb.planes, rb.planes, 9);
+          rb.c3 = pack_conv_bn(p + ".conv3.weight", p + ".bn3", rb.out_planes, rb.planes, 1);
+        } else {
+          rb.c1 = pack_conv_bn(p + ".conv1.weight", p + ".bn1", rb.planes, rb.in_planes, 9);
+          rb.c2 = pack_conv_bn(p + ".conv2.weight", p + ".bn2", rb.planes, rb.planes, 9);
+        }
+        if (rb.has_sc) rb.sc = pack_conv_bn(p + ".shortcut.0.weight", p + ".shortcut.1", rb.out_planes, rb.in_planes, 1);
+      }
+    // seg_1 over TSTP stats; reference flatten index s*C*F4 + c*F4 + f, ours f*2C + s*C + c
+    const int C4 = rblocks.back().out_planes, F4 = feat_dim / 8;
+    const auto& W = P("seg_1.weight");
+    const int K = 2 * C4 * F4;
+    std::vector<float> wp((size_t)embed_dim * K);
+    for (int n = 0; n < embed_dim; ++n)
+      for (int f = 0; f < F4; ++f)
+        for (int sidx = 0; sidx < 2; ++sidx)
+          for (int c = 0; c < C4; ++c)
+            wp[(size_t)n * K + f * 2 * C4 + sidx * C4 + c] = W[(size_t)n * K + sidx * C4 * F4 + c * F4 + f];
+    seg1 = pack_lin(wp.data(), embed_dim, K, K, P("seg_1.bias").data());
+  }
+
+  struct RShapes {
+    size_t big = 0, y1 = 0, y2 = 0, sc = 0;  // floats per utterance
+    int F4 = 0, T4 = 0, C4 = 0;
+  };
+  RShapes resnet_shapes(int T) const {
+    RShapes r;
+    int Fi = feat_dim, Ti = T;
+    r.big = (size_t)Fi * Ti * m_ch;
+    for (const RBlock& rb : rblocks) {
+      const int Fo = (Fi - 1) / rb.stride + 1, To = (Ti - 1) / rb.stride + 1;
+      r.big = std::max(r.big, (size_t)Fo * To * rb.out_planes);
+      r.y1 = std::max(r.y1, (size_t)(bottleneck ? Fi * Ti : Fo * To) * rb.planes);
+      r.y2 = std::max(r.y2, (size_t)Fo * To * rb.planes);
+      if (rb.has_sc) r.sc = std::max(r.sc, (size_t)Fo * To * rb.out_planes);
+      Fi = Fo;
+      Ti = To;
+    }
+    r.F4 = Fi;
+    r.T4 = Ti;
+    r.C4 = rblocks.back().out_planes;
+    return r;
+  }
+  // utterances per forward chunk: every activation operand must stay < 2 GiB
+  // (32-bit buffer-load offsets).
+  int resnet_chunk(int B, int T) const {
+    const RShapes r = resnet_shapes(T);
+    const size_t per = std::max(r.big, std::max(r.y1, std::max(r.y2, r.sc))) * sizeof(float);
+    int bc = (int)std::max<size_t>(1, ((size_t)1 << 31) / 8 * 7 / per);
+    bc = std::min(bc, B);
+    const int chunks = (B + bc - 1) / bc;
+    return (B + chunks - 1) / chunks;
+  }
+  size_t resnet_ws_floats(int B, int T, size_t* offs) const {
+    const int bc = resnet_chunk(B, T);
+    const RShapes r = resnet_shapes(T);
+    const size_t sizes[] = {bc * r.big, bc * r.big, bc * r.y1, bc * r.y2, bc * std::max<size_t>(r.sc, 1),
+                            (size_t)bc * r.F4 * 2 * r.C4};
+    size_t o = 0;
+    for (int i = 0; i < 6; ++i) {
+      if (offs) offs[i] = o;
+      o += (sizes[i] + 63) / 64 * 64;
+    }
+    return o;
+  }
+
+  void gemm2d(const char* tag, const ConvW& cw, const float* a0, int lda, float* out, int ldo, int B,
+              int Fi, int Ti, int kw, int stride, int pad, int act, const float* res, int ldres,
+              hipStream_t s) {
+    ConvGemmArgs g{};
+    g.a[0] = g.a[1] = g.a[2] = a0;
+    g.lda[0] = g.lda[1] = g.lda[2] = lda;
+    g.cseg[0] = 0;
+    g.cseg[1] = g.cseg[2] = g.cseg[3] = cw.cin;
+    const int Fo = (Fi + 2 * pad - kw) / stride + 1, To = (Ti + 2 * pad - kw) / stride + 1;
+    const int M = B * Fo * To;
+    fill(g, cw, M, M, 1, pad, out, ldo, act, nullptr, true);
+    g.conv2d = 1;
+    g.Fi = Fi;
+    g.Ti = Ti;
+    g.Fo = Fo;
+    g.To = To;
+    g.stride = stride;
+    g.kw = kw;
+    g.res = res;
+    g.ldres = ldres;
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, 1, s); });
+  }
+  void gemm1x1(const char* tag, const ConvW& cw, const float* a0, float* out, int M, int act, const float* res,
+               hipStream_t s) {
+    ConvGemmArgs g{};
+    g.a[0] = g.a[1] = g.a[2] = a0;
+    g.lda[0] = g.lda[1] = g.lda[2] = cw.cin;
+    g.cseg[0] = 0;
+    g.cseg[1] = g.cseg[2] = g.cseg[3] = cw.cin;
+    fill(g, cw, M, M, 1, 0, out, cw.N, act, nullptr, true);
+    g.res = res;
+    g.ldres = cw.N;
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, 1, s); });
+  }
+
+  void forward_resnet(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
+    const int bc = resnet_chunk(B, T);
+    size_t off[6];
+    resnet_ws_floats(B, T, off);
+    float* X = ws + off[0];
+    float* O = ws + off[1];
+    float* Y1 = ws + off[2];
+    float* Y2 = ws + off[3];
+    float* SC = ws + off[4];
+    float* pooled = ws + off[5];
+    for (int b0 = 0; b0 < B; b0 += bc) {
+      const int nb = std::min(bc, B - b0);
+      int Fi = feat_dim, Ti = T, Ci = m_ch;
+      run("stem", 0, s, [&] {
+        launch_resnet_stem(feats + (size_t)b0 * T * feat_dim, nb, T, feat_dim, m_ch, stem_w, stem_b, X, s);
+      });
+      float* x = X;
+      float* o = O;
+      for (const RBlock& rb : rblocks) {
+        const int Fo = (Fi - 1) / rb.stride + 1, To = (Ti - 1) / rb.stride + 1;
+        const float* res = x;
+        if (rb.has_sc) {
+          gemm2d("shortcut", rb.sc, x, Ci, SC, rb.out_planes, nb, Fi, Ti, 1, rb.stride, 0, kActNone, nullptr, 0, s);
+          res = SC;
+        }
+        if (bottleneck) {
+          gemm1x1("res_conv1x1", rb.c1, x, Y1, nb * Fi * Ti, kActRelu, nullptr, s);
+          gemm2d("res_conv3x3", rb.c2, Y1, rb.planes, Y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
+          gemm1x1("res_conv1x1", rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
+        } else {
+          gemm2d("res_conv3x3", rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
+          gemm2d("res_conv3x3", rb.c2, Y1, rb.planes, o, rb.out_planes, nb, Fo, To, 3, 1, 1, kActRelu, res,
+                 rb.out_planes, s);
+        }
+        std::swap(x, o);
+        Fi = Fo;
+        Ti = To;
+        Ci = rb.out_planes;
+      }
+      // TSTP over frames for every (utterance, freq) row block, then seg_1
+      run("tstp_head", 0, s, [&] {
+        launch_frame_stats(x, Ci, nb * Fi, Ti, Ci, pooled, 2 * Ci, 1, Ci, s);
+        launch_small_linear({pooled, Fi * 2 * Ci, seg1.wt, seg1.bias, embed + (size_t)b0 * embed_dim, embed_dim, nb,
+                             Fi * 2 * Ci, embed_dim, 0},
+                            s);
+      });
+    }
+  }
+
+  void finalize_ecapa() {
+    const int w = C / 8;
+    layer1 = pack_conv(P("layer1.conv.weight"), C, feat_dim, 5, P("layer1.conv.bias").data(), "layer1.bn");
+    for (int li = 0; li < 3; ++li) {
+      const std::string p = "layer" + std::to_string(li + 2) + ".se_res2block";
+      Block& b = blk[li];
+      b.c1 = pack_conv(P(p + ".0.conv.weight"), C, C, 1, P(p + ".0.conv.bias").data(), p + ".0.bn");
+      for (int i = 0; i < 7; ++i) {
+        const std::string ci = p + ".1.convs." + std::to_string(i);
+        b.res2[i] = pack_conv(P(ci + ".weight"), w, w, 3, P(ci + ".bias").data(),
+                              p + ".1.bns." + std::to_string(i));
+      }
+      b.c3 = pack_conv(P(p + ".2.conv.weight"), C, C, 1, P(p + ".2.conv.bias").data(), p + ".2.bn");
+      b.se1 = pack_lin(P(p + ".3.linear1.weight").data(), 128, C, C, P(p + ".3.linear1.bias").data());
+      b.se2 = pack_lin(P(p + ".3.linear2.weight").data(), C, 128, 128, P(p + ".3.linear2.bias").data());
+    }
+    conv = pack_conv(P("conv.weight"), 1536, 3 * C, 1, P("conv.bias").data(), "");
+    const auto& l1 = P("pool.linear1.weight");
+    const int l1k = glob ? 4608 : 1536;
+    {
+      std::vector<float> wx((size_t)128 * 1536);
+      for (int n = 0; n < 128; ++n)
+        for (int k = 0; k < 1536; ++k) wx[(size_t)n * 1536 + k] = l1[(size_t)n * l1k + k];
+      pool1 = pack_conv(wx, 128, 1536, 1, P("pool.linear1.bias").data(), "");
+      if (glob) {
+        // columns 1536..4607 multiply the (constant over T) mean/std context:
+        // folded into a per-utterance bias computed by small_linear.
+        pool1_ctx = pack_lin(l1.data() + 1536, 128, 3072, l1k, P("pool.linear1.bias").data());
+      }
+    }
+    pool2 = pack_conv(P("pool.linear2.weight"), 1536, 128, 1, P("pool.linear2.bias").data(), "");
+    // head: y = Linear(BN(p)) [-> bn2] folded to y = W' p + b'
+    {
+      std::vector<double> s, t;
+      bn_affine("bn", s, t);
+      const auto& W = P("linear.weight");
+      const auto& bb = P("linear.bias");
+      const int D = embed_dim;
+      std::vector<double> s2(D, 1.0), t2(D, 0.0);
+      if (emb_bn) bn_affine("bn2", s2, t2);
+      std::vector<float> wf((size_t)D * 3072), bf(D);
+      for (int n = 0; n < D; ++n) {
+        double acc = bb[n];
+        for (int k = 0; k < 3072; ++k) {
+          const double wv = W[(size_t)n * 3072 + k];
+          wf[(size_t)n * 3072 + k] = (float)(s2[n] * wv * s[k]);
+          acc += wv * t[k];
+        }
+        bf[n] = (float)(s2[n] * acc + t2[n]);
+      }
+      head = pack_lin(wf.data(), D, 3072, 3072, bf.data());
+    }
+  }
+
+  // --------------------------------------------------------------- launch --
+  template <typename F>
+  void run(const char* tag, double flops, hipStream_t s, F&& f) {
+    if (!prof) {
+      f();
+      return;
+    }
+    ProfEntry& e = prof_map[tag];
+    if (e.used == e.ev.size()) {
+      hipEvent_t a, b;
+      WSP_HIP(hipEventCreate(&a));
+      WSP_HIP(hipEventCreate(&b));
+      e.ev.emplace_back(a, b);
+    }
+    auto& pr = e.ev[e.used++];
+    e.flops = flops;
+    WSP_HIP(hipEventRecord(pr.first, s));
+    f();
+    WSP_HIP(hipEventRecord(pr.second, s));
+  }
+
+  void gemm(const char* tag, const ConvW& cw, const float* a0, int lda, float* out, int ldo, int M,
+            int T, int dil, int pad, int act, hipStream_t s, const float* row_bias = nullptr,
+            bool use_bias = true, int role = 0) {
+    ConvGemmArgs g{};
+    g.role = role;
+    g.a[0] = g.a[1] = g.a[2] = a0;
+    g.lda[0] = g.lda[1] = g.lda[2] = lda;
+    g.cseg[0] = 0;
+    g.cseg[1] = g.cseg[2] = g.cseg[3] = cw.cin;
+    fill(g, cw, M, T, dil, pad, out, ldo, act, row_bias, use_bias);
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch(g, cw, s); });
+  }
+  void launch(const ConvGemmArgs& g, const ConvW& cw, hipStream_t s) {
+    if (precision == 1 && x3_variant == 2 && conv_gemm_dma_supported(g))
+      launch_conv_gemm_dma(g, cw.whi, cw.wlo, s);
+    else if (precision == 1)
+      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 1 : x3_variant, s);
+    else
+      launch_conv_gemm(g, s);
+  }
+  void fill(ConvGemmArgs& g, const ConvW& cw, int M, int T, int dil, int pad, float* out, int ldo,
+            int act, const float* row_bias, bool use_bias) {
+    g.cin = cw.cin;
+    g.taps = cw.taps;
+    g.dil = dil;
+    g.pad = pad;
+    g.M = M;
+    g.T = T;
+    g.N = cw.N;
+    g.w = cw.w;
+    g.K = cw.K;
+    g.Kp = cw.Kp;
+    g.bias = use_bias ? cw.bias : nullptr;
+    g.row_bias = row_bias;
+    g.scale = cw.scale;
+    g.shift = cw.shift;
+    g.out = out;
+    g.ldo = ldo;
+    g.act = act;
+  }
+
+  size_t ecapa_ws_floats(int B, int T, size_t* offs) const {
+    const size_t M = (size_t)B * T;
+    const size_t sizes[] = {M * C, M * C, M * C, M * C,           // x1..x4
+                            M * C, M * C, M * C,                   // h1..h3
+                            (size_t)B * C, (size_t)B * 128, (size_t)B * C,  // gmean, ghid, gate
+                            M * 1536, M * 128, M * 1536,           // xp, att, logit
+                            (size_t)B * 3072, (size_t)B * 128, (size_t)B * 3072};  // gstats, rowb, pooled
+    size_t o = 0;
+    for (int i = 0; i < 16; ++i) {
+      if (offs) offs[i] = o;
+      o += (sizes[i] + 63) / 64 * 64;  // 256-B alignment
+    }
+    return o;
+  }
+
+  void forward_ecapa(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
+    const int M = B * T, w = C / 8;
+    size_t off[16];
+    ecapa_ws_floats(B, T, off);
+    float* x[5] = {nullptr, ws + off[0], ws + off[1], ws + off[2], ws + off[3]};
+    float* h1 = ws + off[4];
+    float* h2 = ws + off[5];
+    float* h3 = ws + off[6];
+    float* gmean = ws + off[7];
+    float* ghid = ws + off[8];
+    float* gate = ws + off[9];
+    float* xp = ws + off[10];
+    float* att = ws + off[11];
+    float* logit = ws + off[12];
+    float* gstats = ws + off[13];
+    float* rowb = ws + off[14];
+    float* pooled = ws + off[15];
+
+    gemm("layer1", layer1, feats, feat_dim, x[1], C, M, T, 1, 2, kActRelu, s);
+    for (int li = 0; li < 3; ++li) {
+      const Block& b = blk[li];
+      const int dil = li + 2;
+      const float* xin = x[li + 1];
+      gemm("conv1x1_CxC", b.c1, xin, C, h1, C, M, T, 1, 0, kActRelu, s, nullptr, true, 1);
+      for (int i = 0; i < 7; ++i) {
+        ConvGemmArgs g{};
+        if (i == 0) {
+          g.amode = kACat;
+          g.a[0] = g.a[1] = g.a[2] = h1;
+          g.lda[0] = g.lda[1] = g.lda[2] = C;
+          g.cseg[0] = 0;
+          g.cseg[1] = g.cseg[2] = g.cseg[3] = w;
+        } else {
+          g.amode = kAAdd;
+          g.a[0] = h1 + i * w;
+          g.a[1] = h2 + (i - 1) * w;
+          g.a[2] = h1;
+          g.lda[0] = g.lda[1] = g.lda[2] = C;
+        }
+        fill(g, b.res2[i], M, T, dil, dil, h2 + i * w, C, kActRelu, nullptr, true);
+        run("res2_k3", 2.0 * M * w * 3 * w, s, [&] { launch(g, b.res2[i], s); });
+      }
+      {
+        ConvGemmArgs g{};
+        g.amode = kACat;
+        g.a[0] = h2;
+        g.a[1] = h1 + 7 * w;
+        g.a[2] = h1;
+        g.lda[0] = g.lda[1] = g.lda[2] = C;
+        g.cseg[0] = 0;
+        g.cseg[1] = 7 * w;
+        g.cseg[2] = g.cseg[3] = C;
+        fill(g, b.c3, M, T, 1, 0, h3, C, kActRelu, nullptr, true);
+        g.role = 1;
+        run("conv1x1_CxC", 2.0 * M * C * C, s, [&] { launch(g, b.c3, s); });
+      }
+      run("se", 0, s, [&] {
+        launch_frame_stats(h3, C, B, T, C, gmean, C, 0, 0, s);
+        launch_small_linear({gmean, C, b.se1.wt, b.se1.bias, ghid, 128, B, C, 128, 1}, s);
+        launch_small_linear({ghid, 128, b.se2.wt, b.se2.bias, gate, C, B, 128, C, 3}, s);
+        launch_residual_scale(xin, h3, gate, x[li + 2], B, T, C, s);
+      });
+    }
+    {
+      ConvGemmArgs g{};
+      g.amode = kACat;
+      g.a[0] = x[2];
+      g.a[1] = x[3];
+      g.a[2] = x[4];
+      g.lda[0] = g.lda[1] = g.lda[2] = C;
+      g.cseg[0] = 0;
+      g.cseg[1] = C;
+      g.cseg[2] = 2 * C;
+      g.cseg[3] = 3 * C;
+      fill(g, conv, M, T, 1, 0, xp, 1536, kActRelu, nullptr, true);
+      run("conv_cat", 2.0 * M * 1536 * 3 * C, s, [&] { launch(g, conv, s); });
+    }
+    if (glob) {
+      run("glob_ctx", 0, s, [&] {
+        launch_frame_stats(xp, 1536, B, T, 1536, gstats, 3072, 1, 1536, s);
+        launch_small_linear({gstats, 3072, pool1_ctx.wt, pool1_ctx.bias, rowb, 128, B, 3072, 128, 0}, s);
+      });
+      gemm("pool_linear1", pool1, xp, 1536, att, 128, M, T, 1, 0, kActTanh, s, rowb, false);
+    } else {
+      gemm("pool_linear1", pool1, xp, 1536, att, 128, M, T, 1, 0, kActTanh, s);
+    }
+    gemm("pool_linear2", pool2, att, 128, logit, 1536, M, T, 1, 0, kActNone, s);
+    run("astp", 0, s, [&] { launch_astp_pool(logit, xp, B, T, 1536, pooled, s); });
+    run("head", 0, s, [&] {
+      launch_small_linear({pooled, 3072, head.wt, head.bias, embed, embed_dim, B, 3072, embed_dim, 0}, s);
+    });
+  }
+};
+
+}  // namespace wsp

@@ -29,36 +29,44 @@ def _to_numpy(v) -> np.ndarray:
     return a if a.flags.c_contiguous else a.copy()  # (ascontiguousarray turns 0-d into 1-d)
 
 
-class HipSpeakerModel:
-    """ECAPA-TDNN / ResNet speaker backbone executed by hand-written gfx950 kernels."""
+class _HipHandle:
+    """Weight intake + device handle shared by the speaker backbones and the
+    SSL front end: reference state_dict names in, one `wsp_model` handle per
+    device out.  Subclasses provide `_layout`, `_create_args()` and
+    `_ignored_keys` (checkpoint entries the reference module holds but the
+    extraction path never reads)."""
 
-    def __init__(self, arch: str, **model_args):
-        self.spec: ModelSpec = make_spec(arch, **model_args)
-        if self.spec.two_emb_layer:
-            raise NotImplementedError("two_emb_layer=True is not implemented on the HIP path")
-        self._layout = param_list(self.spec)
+    _ignored_prefixes: Tuple[str, ...] = ()
+
+    def __init__(self):
         self._host: Dict[str, np.ndarray] = {}
         self._handle: Optional[ctypes.c_void_p] = None
         self._device: Optional[int] = None
         self._ws: Optional[torch.Tensor] = None
         self._options: Dict[str, int] = {}
+        self._pre_finalize: Tuple[str, ...] = ()
 
     # ----------------------------------------------------------- weights --
     def state_dict_layout(self) -> List[Tuple[str, Tuple[int, ...]]]:
         return list(self._layout)
+
+    def _canonical(self, key: str) -> str:
+        return key
 
     def load_state_dict(self, state_dict, strict: bool = False):
         """Mirror of `model.load_state_dict(checkpoint, strict=False)` + its warnings."""
         names = {n: s for n, s in self._layout}
         missing, unexpected = [], []
         for k, v in state_dict.items():
-            if k not in names:
-                unexpected.append(k)
+            key = self._canonical(k)
+            if key not in names:
+                if not any(key.startswith(p) for p in self._ignored_prefixes):
+                    unexpected.append(k)
                 continue
             arr = _to_numpy(v)
-            if tuple(arr.shape) != tuple(names[k]):
-                raise ValueError(f"size mismatch for {k}: {tuple(arr.shape)} vs {names[k]}")
-            self._host[k] = arr
+            if tuple(arr.shape) != tuple(names[key]):
+                raise ValueError(f"size mismatch for {k}: {tuple(arr.shape)} vs {names[key]}")
+            self._host[key] = arr
         for n, _ in self._layout:
             if n not in self._host:
                 missing.append(n)
@@ -90,7 +98,7 @@ class HipSpeakerModel:
     def to(self, device):
         device = torch.device(device)
         if device.type != "cuda":
-            raise RuntimeError("HipSpeakerModel runs only on a HIP device (no CPU fallback)")
+            raise RuntimeError(f"{type(self).__name__} runs only on a HIP device (no CPU fallback)")
         idx = device.index if device.index is not None else torch.cuda.current_device()
         if self._handle is None or self._device != idx:
             self._release()
@@ -102,14 +110,16 @@ class HipSpeakerModel:
     def _build(self):
         lib = _lib.load()
         h = ctypes.c_void_p()
-        s = self.spec
-        _lib.check(lib.wsp_model_create(s.arch.encode(), s.feat_dim, s.embed_dim, int(s.emb_bn),
-                                        int(s.two_emb_layer), ctypes.byref(h)), "wsp_model_create")
+        arch, feat_dim, embed_dim, emb_bn, two_emb = self._create_args()
+        _lib.check(lib.wsp_model_create(arch.encode(), feat_dim, embed_dim, int(emb_bn), int(two_emb),
+                                        ctypes.byref(h)), "wsp_model_create")
         n = lib.wsp_model_num_params(h)
         name = ctypes.c_char_p()
         ndim = ctypes.c_int()
         shape = (ctypes.c_int64 * 4)()
         try:
+            for k in self._pre_finalize:
+                _lib.check(lib.wsp_model_set_option(h, k.encode(), self._options[k]), "set_option " + k)
             for i in range(n):
                 _lib.check(lib.wsp_model_param_info(h, i, ctypes.byref(name), ctypes.byref(ndim), shape),
                            "param_info")
@@ -125,11 +135,58 @@ class HipSpeakerModel:
                 _lib.check(lib.wsp_model_set_param(h, i, arr.ctypes.data, arr.size), "set_param " + key)
             _lib.check(lib.wsp_model_finalize(h), "wsp_model_finalize")
             for k, v in self._options.items():
-                _lib.check(lib.wsp_model_set_option(h, k.encode(), v), "set_option " + k)
+                if k not in self._pre_finalize:
+                    _lib.check(lib.wsp_model_set_option(h, k.encode(), v), "set_option " + k)
         except Exception:
             lib.wsp_model_destroy(h)
             raise
         self._handle = h
+
+    def _need(self):
+        if self._handle is None:
+            raise RuntimeError("model not on a HIP device: call .to('cuda') first")
+
+    def _workspace_tensor(self, need: int, device) -> torch.Tensor:
+        if self._ws is None or self._ws.numel() < need or self._ws.device != device:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=device)
+        return self._ws
+
+    def set_option(self, key: str, value: int):
+        """'precision': 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA."""
+        self._options[key] = int(value)
+        if key in self._pre_finalize:
+            self._release()  # rebuilt with the option on the next .to()/forward
+        elif self._handle is not None:
+            _lib.check(_lib.load().wsp_model_set_option(self._handle, key.encode(), int(value)), "set_option")
+
+    # ----------------------------------------------------------- profile --
+    def profile(self, enable: bool):
+        self._need()
+        _lib.check(_lib.load().wsp_model_profile(self._handle, int(enable)), "profile")
+
+    def profile_query(self, kernel_class: str):
+        self._need()
+        n = ctypes.c_int()
+        ms = ctypes.c_double()
+        fl = ctypes.c_double()
+        _lib.check(_lib.load().wsp_model_profile_query(self._handle, kernel_class.encode(), ctypes.byref(n),
+                                                       ctypes.byref(ms), ctypes.byref(fl)), "profile_query")
+        return n.value, ms.value, fl.value
+
+
+class HipSpeakerModel(_HipHandle):
+    """ECAPA-TDNN / ResNet speaker backbone executed by hand-written gfx950 kernels."""
+
+    def __init__(self, arch: str, **model_args):
+        super().__init__()
+        self.spec: ModelSpec = make_spec(arch, **model_args)
+        if self.spec.two_emb_layer:
+            raise NotImplementedError("two_emb_layer=True is not implemented on the HIP path")
+        self._layout = param_list(self.spec)
+
+    def _create_args(self):
+        s = self.spec
+        return s.arch, s.feat_dim, s.embed_dim, s.emb_bn, s.two_emb_layer
 
     # ----------------------------------------------------------- forward --
     def workspace_bytes(self, B: int, T: int) -> int:
@@ -139,15 +196,8 @@ class HipSpeakerModel:
                    "workspace_bytes")
         return b.value
 
-    def _need(self):
-        if self._handle is None:
-            raise RuntimeError("model not on a HIP device: call .to('cuda') first")
-
     def _workspace(self, B: int, T: int, device) -> torch.Tensor:
-        need = self.workspace_bytes(B, T)
-        if self._ws is None or self._ws.numel() < need or self._ws.device != device:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=device)
-        return self._ws
+        return self._workspace_tensor(self.workspace_bytes(B, T), device)
 
     def embed(self, feats: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """(B, T, feat_dim) float32 cuda -> (B, embed_dim) float32 cuda."""
@@ -171,26 +221,6 @@ class HipSpeakerModel:
         return None, self.embed(feats)
 
     forward = __call__
-
-    def set_option(self, key: str, value: int):
-        """'precision': 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA."""
-        self._options[key] = int(value)
-        if self._handle is not None:
-            _lib.check(_lib.load().wsp_model_set_option(self._handle, key.encode(), int(value)), "set_option")
-
-    # ----------------------------------------------------------- profile --
-    def profile(self, enable: bool):
-        self._need()
-        _lib.check(_lib.load().wsp_model_profile(self._handle, int(enable)), "profile")
-
-    def profile_query(self, kernel_class: str):
-        self._need()
-        n = ctypes.c_int()
-        ms = ctypes.c_double()
-        fl = ctypes.c_double()
-        _lib.check(_lib.load().wsp_model_profile_query(self._handle, kernel_class.encode(), ctypes.byref(n),
-                                                       ctypes.byref(ms), ctypes.byref(fl)), "profile_query")
-        return n.value, ms.value, fl.value
 
 
 def get_speaker_model(model_name: str):
