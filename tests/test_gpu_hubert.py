@@ -65,7 +65,7 @@ def test_hidden_state_matches_oracle(sd_np, sd_t, layer):
 
 
 @pytest.mark.parametrize("precision", [1, 0], ids=["bf16x3", "f32"])
-@pytest.mark.parametrize("W", [16000, 12345, 400])
+@pytest.mark.parametrize("W", [16000, 12345, 400, 48000])
 def test_featurizer_output_matches_oracle(sd_np, sd_t, precision, W):
     wav = _wav(8, 2, W)
     fe = _frontend(sd_np, precision=precision)

@@ -8,8 +8,8 @@
 //        pass instead of round-tripping 33 MB/utt of pre-norm activations)
 //   layernorm  : rows of D in {512, 768}, optional (remapped) residual add,
 //                optional s3prl Featurizer accumulation + length match
-//   mha        : softmax(QK^T/8) V per (utterance, head), online softmax over
-//                64-key blocks staged in LDS (T = 249 frames for 5 s)
+//   mha        : softmax(QK^T/8) V per (utterance, head) on bf16x3 MFMA, online
+//                softmax over 32-key chunks staged in LDS (T = 249 frames for 5 s)
 //   cmn_rows   : per-utterance mean removal over frames (dataset_utils.py:19-26)
 #include <cfloat>
 
@@ -127,126 +127,185 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LayerNormArgs p) {
 }
 
 // ------------------------------------------------------------------ mha ---
-// One block = (64 queries, head, utterance); thread (q = tid/4, sub = tid%4)
-// scores keys 4j+sub of each 64-key block and owns output dims 16 sub..+15.
-constexpr int kDH = 64, kQB = 64, kKB = 64, kLD = kDH + 4;
+// softmax(Q K^T / 8) V on bf16x3 MFMA (fp32-class: every product is
+// a_hi*b_hi + a_hi*b_lo + a_lo*b_hi with fp32 accumulation).
+// Block = (128 queries, head, utterance), 4 waves x 32 queries; keys stream in
+// 32-key chunks through a double-buffered LDS ring (K as [key][d], V as
+// V^T [d][key]), the next chunk's global loads in flight during the current
+// chunk's MFMAs.  Per chunk each wave computes S^T = K_c Q^T (32 keys x 32
+// queries: query on the lane, keys in the accumulator registers), an online
+// softmax per lane-column, then O^T += V_c^T P with P taken straight from the
+// S^T accumulator registers (cdna_hip_programming.md §3: an accumulator tile
+// as the next MFMA's B operand, k order 16s + 8(j>>2) + 4h + (j&3)).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kDH = 64, kQW = 32, kWaves = 4, kKC = 32;
+constexpr int kKLD = kDH + 4;  // Ks row stride (floats): conflict-free ds_read_b128 over 32 key rows
+constexpr int kVLD = kKC + 4;  // VTs row stride (floats)
+
+__device__ __forceinline__ void split8(const f32x4 a, const f32x4 b, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 h0 = (__bf16)a[e], h1 = (__bf16)b[e];
+    hi[e] = h0;
+    hi[e + 4] = h1;
+    lo[e] = (__bf16)(a[e] - (float)h0);
+    lo[e + 4] = (__bf16)(b[e] - (float)h1);
+  }
+}
+
+__device__ __forceinline__ f32x16 mma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
+                                       f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
+}
 
 __global__ __launch_bounds__(256) void mha_kernel(const float* __restrict__ qkv, int ldq, float* __restrict__ out,
                                                   int ldo, int T, int D, float scale) {
-  __shared__ __attribute__((aligned(16))) float Ks[kKB * kLD];
-  __shared__ __attribute__((aligned(16))) float Vs[kKB * kLD];
-  __shared__ __attribute__((aligned(16))) float Ps[kQB * kLD];
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * kQB;
-  const int tid = threadIdx.x, qi = tid >> 2, sub = tid & 3;
-  const int tq = q0 + qi;
+  __shared__ __attribute__((aligned(16))) float Ks[2][kKC * kKLD];
+  __shared__ __attribute__((aligned(16))) float VTs[2][kDH * kVLD];
+  const int b = blockIdx.z, head = blockIdx.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int q = blockIdx.x * (kQW * kWaves) + wave * kQW + r;
   const float* base = qkv + (size_t)b * T * ldq;
-  float q[kDH];
+  const float* kbase = base + D + head * kDH;
+  const float* vbase = base + 2 * D + head * kDH;
+
+  // Q^T fragments (B operand of S^T = K Q^T): lane = query r, d = 16s + 8hh + j; pre-scaled by
+  // 1/sqrt(dh) = 1/8 (exact in binary).
+  bf16x8 qh[4], ql[4];
   {
-    const float* qr = base + (size_t)min(tq, T - 1) * ldq + h * kDH;
+    const float* qr = base + (size_t)min(q, T - 1) * ldq + head * kDH + 8 * hh;
+    const float sc = q < T ? scale : 0.f;
 #pragma unroll
-    for (int d = 0; d < kDH; d += 4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(qr + d);
-      q[d] = v[0] * scale;
-      q[d + 1] = v[1] * scale;
-      q[d + 2] = v[2] * scale;
-      q[d + 3] = v[3] * scale;
+    for (int s = 0; s < 4; ++s) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(qr + 16 * s) * sc;
+      const f32x4 c = *reinterpret_cast<const f32x4*>(qr + 16 * s + 4) * sc;
+      split8(a, c, qh[s], ql[s]);
     }
   }
-  float m = -FLT_MAX, l = 0.f, o[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) o[i] = 0.f;
 
-  for (int k0 = 0; k0 < T; k0 += kKB) {
-    __syncthreads();
+  // chunk staging: 2 float4 of K and 2 of V per thread (32 keys x 64 d each)
+  f32x4 kr[2], vr[2];
+  auto load_chunk = [&](int c) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = tid + 256 * i;
-      const int r = f >> 4, c4 = (f & 15) * 4;
-      const int tk = k0 + r;
-      f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
-      if (tk < T) {
-        kv = *reinterpret_cast<const f32x4*>(base + (size_t)tk * ldq + D + h * kDH + c4);
-        vv = *reinterpret_cast<const f32x4*>(base + (size_t)tk * ldq + 2 * D + h * kDH + c4);
-      }
-      *reinterpret_cast<f32x4*>(Ks + r * kLD + c4) = kv;
-      *reinterpret_cast<f32x4*>(Vs + r * kLD + c4) = vv;
+    for (int i = 0; i < 2; ++i) {
+      const int f = tid + 256 * i, key = c * kKC + (f >> 4), d4 = (f & 15) * 4;
+      const bool ok = key < T;
+      const size_t off = (size_t)(ok ? key : 0) * ldq + d4;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      kr[i] = ok ? *reinterpret_cast<const f32x4*>(kbase + off) : z;
+      vr[i] = ok ? *reinterpret_cast<const f32x4*>(vbase + off) : z;
     }
-    __syncthreads();
-    float s[16];
-    float bm = -FLT_MAX;
+  };
+  auto store_chunk = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int kr = 4 * j + sub;
-      const float* kp = Ks + kr * kLD;
-      float a0 = 0.f, a1 = 0.f;
+    for (int i = 0; i < 2; ++i) {
+      const int f = tid + 256 * i, key = f >> 4, d4 = (f & 15) * 4;
+      *reinterpret_cast<f32x4*>(&Ks[buf][key * kKLD + d4]) = kr[i];
 #pragma unroll
-      for (int d = 0; d < kDH; d += 8) {
-        const f32x4 x0 = *reinterpret_cast<const f32x4*>(kp + d);
-        const f32x4 x1 = *reinterpret_cast<const f32x4*>(kp + d + 4);
-        a0 = fmaf(q[d], x0[0], a0);
-        a0 = fmaf(q[d + 1], x0[1], a0);
-        a0 = fmaf(q[d + 2], x0[2], a0);
-        a0 = fmaf(q[d + 3], x0[3], a0);
-        a1 = fmaf(q[d + 4], x1[0], a1);
-        a1 = fmaf(q[d + 5], x1[1], a1);
-        a1 = fmaf(q[d + 6], x1[2], a1);
-        a1 = fmaf(q[d + 7], x1[3], a1);
-      }
-      s[j] = (k0 + kr < T) ? a0 + a1 : -FLT_MAX;
-      bm = fmaxf(bm, s[j]);
+      for (int e = 0; e < 4; ++e) VTs[buf][(d4 + e) * kVLD + key] = vr[i][e];
     }
-    bm = fmaxf(bm, __shfl_xor(bm, 1, 64));
-    bm = fmaxf(bm, __shfl_xor(bm, 2, 64));
-    const float mn = fmaxf(m, bm);
+  };
+
+  f32x16 o[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[t][e] = 0.f;
+  float m = -FLT_MAX, l = 0.f;
+
+  const int nch = (T + kKC - 1) / kKC;
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nch) load_chunk(c + 1);
+    // S^T (32 keys x 32 queries)
+    f32x16 st;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) st[e] = 0.f;
+    const float* kp = &Ks[buf][r * kKLD + 8 * hh];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 kh, kl;
+      split8(*reinterpret_cast<const f32x4*>(kp + 16 * s), *reinterpret_cast<const f32x4*>(kp + 16 * s + 4), kh, kl);
+      st = mma3(kh, kl, qh[s], ql[s], st);
+    }
+    // online softmax over the keys of this lane's query column
+    float cmax = -FLT_MAX;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int key = c * kKC + (e & 3) + 8 * (e >> 2) + 4 * hh;
+      if (key >= T) st[e] = -FLT_MAX;
+      cmax = fmaxf(cmax, st[e]);
+    }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    const float mn = fmaxf(m, cmax);
     const float corr = expf(m - mn);
     float ls = 0.f;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float pj = (k0 + 4 * j + sub < T) ? expf(s[j] - mn) : 0.f;
-      ls += pj;
-      Ps[qi * kLD + 4 * j + sub] = pj;
+    for (int e = 0; e < 16; ++e) {
+      const int key = c * kKC + (e & 3) + 8 * (e >> 2) + 4 * hh;
+      const float pe = key < T ? expf(st[e] - mn) : 0.f;
+      st[e] = pe;
+      ls += pe;
     }
-    ls += __shfl_xor(ls, 1, 64);
-    ls += __shfl_xor(ls, 2, 64);
     l = l * corr + ls;
     m = mn;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) o[i] *= corr;
-    __syncthreads();
-    const int kn = min(kKB, T - k0);
-    for (int kk = 0; kk < kn; ++kk) {
-      const float pv = Ps[qi * kLD + kk];
-      const float* vp = Vs + kk * kLD + sub * 16;
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 16; i += 4) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(vp + i);
-        o[i] = fmaf(pv, v[0], o[i]);
-        o[i + 1] = fmaf(pv, v[1], o[i + 1]);
-        o[i + 2] = fmaf(pv, v[2], o[i + 2]);
-        o[i + 3] = fmaf(pv, v[3], o[i + 3]);
+      for (int e = 0; e < 16; ++e) o[t][e] *= corr;
+    // O^T (64 d x 32 queries) += V_c^T P
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 ph, pl;
+      const f32x4 p0 = {st[8 * s], st[8 * s + 1], st[8 * s + 2], st[8 * s + 3]};
+      const f32x4 p1 = {st[8 * s + 4], st[8 * s + 5], st[8 * s + 6], st[8 * s + 7]};
+      split8(p0, p1, ph, pl);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float* vp = &VTs[buf][(32 * t + r) * kVLD + 16 * s + 4 * hh];
+        bf16x8 vh, vl;
+        split8(*reinterpret_cast<const f32x4*>(vp), *reinterpret_cast<const f32x4*>(vp + 8), vh, vl);
+        o[t] = mma3(vh, vl, ph, pl, o[t]);
       }
     }
+    if (c + 1 < nch) store_chunk(buf ^ 1);
+    __syncthreads();
   }
-  if (tq < T) {
-    const float inv = 1.f / l;
-    float* op = out + ((size_t)b * T + tq) * ldo + h * kDH + sub * 16;
+  const float inv = 1.f / (l + __shfl_xor(l, 32, 64));
+  if (q < T) {
+    float* op = out + ((size_t)b * T + q) * ldo + head * kDH + 4 * hh;
 #pragma unroll
-    for (int i = 0; i < 16; i += 4) {
-      const f32x4 v = {o[i] * inv, o[i + 1] * inv, o[i + 2] * inv, o[i + 3] * inv};
-      *reinterpret_cast<f32x4*>(op + i) = v;
-    }
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = {o[t][4 * g] * inv, o[t][4 * g + 1] * inv, o[t][4 * g + 2] * inv, o[t][4 * g + 3] * inv};
+        *reinterpret_cast<f32x4*>(op + 32 * t + 8 * g) = v;
+      }
   }
 }
 
 // ------------------------------------------------------------- cmn_rows ---
+// Block = (64 channels, utterance); 4 row groups of 64 lanes: coalesced
+// 256-B row segments, partial sums combined through LDS.
 __global__ __launch_bounds__(256) void cmn_rows_kernel(float* __restrict__ x, int T, int D) {
-  const int b = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= D) return;
+  __shared__ float part[4][64];
+  const int b = blockIdx.y, c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
   float* p = x + (size_t)b * T * D + c;
   float s = 0.f;
-  for (int t = 0; t < T; ++t) s += p[(size_t)t * D];
-  const float mean = s / (float)T;
-  for (int t = 0; t < T; ++t) p[(size_t)t * D] -= mean;
+  if (c < D)
+    for (int t = g; t < T; t += 4) s += p[(size_t)t * D];
+  part[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  const float mean = (part[0][threadIdx.x & 63] + part[1][threadIdx.x & 63] + part[2][threadIdx.x & 63] +
+                      part[3][threadIdx.x & 63]) / (float)T;
+  if (c < D)
+    for (int t = g; t < T; t += 4) p[(size_t)t * D] -= mean;
 }
 
 }  // namespace
@@ -278,14 +337,14 @@ void launch_layernorm(const LayerNormArgs& p, hipStream_t s) {
 void launch_mha(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s) {
   WSP_CHECK(dh == kDH, "mha: head dim must be 64");
   WSP_CHECK(B > 0 && T > 0 && H > 0 && ldq >= 3 * H * dh && ldq % 4 == 0 && ldo % 4 == 0, "mha: bad shape");
-  const dim3 grid((T + kQB - 1) / kQB, H, B);
+  const dim3 grid((T + kQW * kWaves - 1) / (kQW * kWaves), H, B);
   hipLaunchKernelGGL(mha_kernel, grid, dim3(256), 0, s, qkv, ldq, out, ldo, T, H * dh, 1.f / sqrtf((float)dh));
   WSP_HIP(hipGetLastError());
 }
 
 void launch_cmn_rows(float* x, int B, int T, int D, hipStream_t s) {
   WSP_CHECK(B > 0 && T > 0 && D > 0, "cmn: bad shape");
-  hipLaunchKernelGGL(cmn_rows_kernel, dim3((D + 255) / 256, B), dim3(256), 0, s, x, T, D);
+  hipLaunchKernelGGL(cmn_rows_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, x, T, D);
   WSP_HIP(hipGetLastError());
 }
 
