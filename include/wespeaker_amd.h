@@ -106,7 +106,8 @@ int wsp_model_forward(wsp_model* m, const float* feats, int B, int T, float* emb
  *   "precision"  1 = bf16x3 split MFMA (default; fp32-class accuracy),
  *                0 = exact f32 MFMA
  *   "x3_variant" bf16x3 block tile: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves),
- *                2 = LDS-DMA staged 256x128 where supported
+ *                2 = LDS-DMA staged 256x128 where supported, 3 = 128x128 with
+ *                swizzled 64-B LDS rows, 4 = 256x128 swizzled (default)
  *   "layer"      HuBERT front end only, before finalize: -1 = weighted sum of all
  *                hidden states (default), k = hidden state k alone (s3prl.py:84-87) */
 int wsp_model_set_option(wsp_model* m, const char* key, int value);

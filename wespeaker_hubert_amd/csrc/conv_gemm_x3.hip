@@ -27,12 +27,27 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 32;
-constexpr int ROWB = 80;  // bytes per LDS row (32 bf16 + 8 pad)
 
-template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D = false>
+// LDS row layout of one 32-wide k-tile row (bf16): padded 80-B rows, or
+// unpadded 64-B rows with the 16-B chunk XOR-swizzled by (row >> 2) & 3 —
+// both conflict-free for the fragment reads (row = lane & 31, chunk = 2s + h);
+// the swizzled form is 20 % smaller (two 128 x 128 blocks fit a CU).
+template <bool SWZ>
+struct Lds {
+  static constexpr int ROWB = SWZ ? 64 : 80;
+  static constexpr int SKEW = SWZ ? 0 : 64;  // lo W image offset (padded rows: 16-bank skew)
+  __device__ __forceinline__ static int off(int row, int byte) {
+    if constexpr (SWZ) return row * 64 + ((((byte >> 4) ^ (row >> 2)) & 3) << 4) + (byte & 15);
+    else return row * 80 + byte;
+  }
+};
+
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D = false, bool SWZ = false>
 __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArgs p,
                                                                const __bf16* __restrict__ whi,
                                                                const __bf16* __restrict__ wlo) {
+  using L = Lds<SWZ>;
+  constexpr int ROWB = L::ROWB;
   constexpr int NT = WM * WN * 64;
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
@@ -41,7 +56,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   constexpr int ROWS_A = NT / 8;        // A rows covered per pass
   constexpr int A_BYTES = BM * ROWB;    // one bf16 image (hi or lo) of the A tile
   constexpr int B_BYTES = BN * ROWB;
-  constexpr int B_LO = B_BYTES + 64;  // lo image skewed by 16 banks vs hi (conflict-free stores)
+  constexpr int B_LO = B_BYTES + L::SKEW;
   constexpr int STAGE = 2 * A_BYTES + B_LO + B_BYTES;
   static_assert(AR >= 1 && BR >= 1, "tile too small for the thread count");
   static_assert(BN * 4 % 64 == 0, "a W image must be a whole number of wave loads");
@@ -79,7 +94,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
     const int row = qq >> 2, part = qq & 3;
     bimg[i] = img != 0;
     boff[i] = ((n0 + row) * p.Kp + part * 8) * 2;
-    bls[i] = row * ROWB + part * 16 + (img ? B_LO : 0);
+    bls[i] = L::off(row, part * 16) + (img ? B_LO : 0);
   }
 
   // Two register sets: tile k+1 is converted and written to LDS while tile k
@@ -109,7 +124,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
         hi[e] = hh;
         lo[e] = (__bf16)(x - (float)hh);
       }
-      const int off = (srow + ROWS_A * i) * ROWB + c4 * 2;
+      const int off = L::off(srow + ROWS_A * i, c4 * 2);
       *reinterpret_cast<bf16x4*>(st + off) = hi;
       *reinterpret_cast<bf16x4*>(st + A_BYTES + off) = lo;
     }
@@ -132,9 +147,9 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
 
   auto mma_step = [&](int buf, int s) {
     const unsigned char* st = smem + buf * STAGE;
-    const unsigned char* a_hi = st + (wm * TM * 32 + r32) * ROWB + h * 16 + s * 32;
+    const unsigned char* a_hi = st + L::off(wm * TM * 32 + r32, h * 16 + s * 32);
     const unsigned char* a_lo = a_hi + A_BYTES;
-    const unsigned char* b_hi = st + 2 * A_BYTES + (wn * TN * 32 + r32) * ROWB + h * 16 + s * 32;
+    const unsigned char* b_hi = st + 2 * A_BYTES + L::off(wn * TN * 32 + r32, h * 16 + s * 32);
     const unsigned char* b_lo = b_hi + B_LO;
     bf16x8 ah[TM], al_[TM], bh[TN], bl[TN];
 #pragma unroll
@@ -185,34 +200,35 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   gemm_epilogue<TM, TN>(p, acc, m0, n0, wm, wn, lane);
 }
 
-template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D = false>
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D, bool SWZ>
 void launch_x3_k(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
+  constexpr int ROWB = Lds<SWZ>::ROWB;
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
-  const size_t lds = (size_t)2 * (2 * BM * ROWB + 2 * BN * ROWB + 64);
-  hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, AMODE, UNI, ROLE, C2D>), dim3(nwg), dim3(NT), lds, s,
+  const size_t lds = (size_t)2 * (2 * BM * ROWB + 2 * BN * ROWB + Lds<SWZ>::SKEW);
+  hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, AMODE, UNI, ROLE, C2D, SWZ>), dim3(nwg), dim3(NT), lds, s,
                      p, whi, wlo);
   WSP_HIP(hipGetLastError());
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, bool SWZ = false>
 void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
   if (p.conv2d) {
-    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, true>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, true, SWZ>(p, whi, wlo, s);
     return;
   }
   const bool uni = uniform_ktiles(p);
   if (p.amode == kAAdd) {
     if (uni)
-      launch_x3_k<WM, WN, TM, TN, kAAdd, true, 0>(p, whi, wlo, s);
+      launch_x3_k<WM, WN, TM, TN, kAAdd, true, 0, false, SWZ>(p, whi, wlo, s);
     else
-      launch_x3_k<WM, WN, TM, TN, kAAdd, false, 0>(p, whi, wlo, s);
+      launch_x3_k<WM, WN, TM, TN, kAAdd, false, 0, false, SWZ>(p, whi, wlo, s);
   } else if (!uni) {
-    launch_x3_k<WM, WN, TM, TN, kACat, false, 0>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, false, 0, false, SWZ>(p, whi, wlo, s);
   } else if (p.role == 1) {
-    launch_x3_k<WM, WN, TM, TN, kACat, true, 1>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 1, false, SWZ>(p, whi, wlo, s);
   } else {
-    launch_x3_k<WM, WN, TM, TN, kACat, true, 0>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, false, SWZ>(p, whi, wlo, s);
   }
 }
 
@@ -233,6 +249,10 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
     launch_x3_tile<4, 1, 1, 2>(p, h, l, s);  // 128 x 64, 4 waves
   } else if (variant == 1) {
     launch_x3_tile<4, 2, 2, 2>(p, h, l, s);  // 256 x 128, 8 waves
+  } else if (variant == 3) {
+    launch_x3_tile<2, 2, 2, 2, true>(p, h, l, s);  // 128 x 128, 4 waves, swizzled rows: 2 blocks / CU
+  } else if (variant == 4) {
+    launch_x3_tile<4, 2, 2, 2, true>(p, h, l, s);  // 256 x 128, 8 waves, swizzled rows
   } else {
     launch_x3_tile<2, 2, 2, 2>(p, h, l, s);  // 128 x 128, 4 waves
   }

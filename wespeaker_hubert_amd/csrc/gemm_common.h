@@ -194,9 +194,11 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
   const int h = lane >> 5;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
   if (p.res) {
+    // one 32-row tile at a time: TN*16 residual loads in flight (register budget)
     const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res);
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      float rv[TN][16];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + (wn * TN + j) * 32 + r32;
@@ -204,9 +206,14 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + (wm * TM + i) * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
           const int off = row < p.M ? (row * p.ldres + col) * 4 : kOOB;
-          acc[i][j][r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, off, 0, 0));
+          rv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, off, 0, 0));
         }
       }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] += rv[j][r];
+    }
   }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {

@@ -61,7 +61,9 @@ inline ConvGemmArgs normalized(ConvGemmArgs p) {
 }
 
 // bf16x3 split-precision variant (conv_gemm_x3.hip); whi/wlo = packed [N][Kp]
-// bf16 hi/lo images of W.  variant: 0 = 128x128/4 waves, 1 = 256x128/8 waves.
+// bf16 hi/lo images of W.  variant (N % 128 == 0): 0 = 128x128/4 waves,
+// 1 = 256x128/8 waves, 3 = 128x128 swizzled LDS rows (2 blocks/CU),
+// 4 = 256x128 swizzled LDS rows (default).
 void launch_conv_gemm_x3(const ConvGemmArgs& p, const void* whi, const void* wlo, int variant,
                          hipStream_t s);
 

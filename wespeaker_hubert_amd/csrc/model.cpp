@@ -144,7 +144,7 @@ void Model::set_option(const std::string& key, int value) {
     WSP_CHECK(value >= -1 && value <= 12, "layer must be -1 (weighted sum) or 0..12");
     impl->h_layer_sel = value;
   } else if (key == "x3_variant") {
-    WSP_CHECK(value >= 0 && value <= 2, "x3_variant must be 0, 1 or 2");
+    WSP_CHECK(value >= 0 && value <= 4, "x3_variant must be 0..4");
     impl->x3_variant = value;
   } else {
     throw InvalidArg{"unknown option " + key};

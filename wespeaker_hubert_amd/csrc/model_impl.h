@@ -161,7 +161,7 @@ struct Model::Impl {
 
   // 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA
   int precision = 1;
-  int x3_variant = 1;
+  int x3_variant = 4;  // 256 x 128 swizzled-LDS bf16x3 tiles (tools/gemm_bench: +3-8 % over 1)
 
   // profiling
   bool prof = false;
@@ -447,7 +447,7 @@ struct Model::Impl {
     g.kw = kw;
     g.res = res;
     g.ldres = ldres;
-    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, 1, s); });
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 4 : x3_variant, s); });
   }
   void gemm1x1(const char* tag, const ConvW& cw, const float* a0, float* out, int M, int act, const float* res,
                hipStream_t s) {
@@ -459,7 +459,7 @@ struct Model::Impl {
     fill(g, cw, M, M, 1, 0, out, cw.N, act, nullptr, true);
     g.res = res;
     g.ldres = cw.N;
-    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, 1, s); });
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 4 : x3_variant, s); });
   }
 
   void forward_resnet(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
@@ -602,7 +602,7 @@ struct Model::Impl {
     if (precision == 1 && x3_variant == 2 && conv_gemm_dma_supported(g))
       launch_conv_gemm_dma(g, cw.whi, cw.wlo, s);
     else if (precision == 1)
-      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 1 : x3_variant, s);
+      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 4 : x3_variant, s);
     else
       launch_conv_gemm(g, s);
   }
