@@ -185,3 +185,41 @@ def test_scoring_pipeline_matches_oracle(tmp_path):
     lab = np.array([x.split()[3] == "target" for x in lines])
     fnr, fpr = scoring_ref.compute_pmiss_pfa_rbst(sc, lab)
     assert abs(eer - 100 * scoring_ref.compute_eer(fnr, fpr)) < 1e-9
+
+
+def test_extract_driver_s3prl_hubert(wav_scp, tmp_path):
+    """bin/extract.py with a reference-style SSL config (ecapa_tdnn_WavLM_frozen.yaml shape,
+    upstream hubert_base): checkpoint = backbone + frontend.* entries; whole utterances,
+    [-1,1] audio -> HuBERT -> featurizer -> CMN -> ECAPA_TDNN_GLOB_c512(768)."""
+    from oracle import hubert_ref
+    from wespeaker_hubert_amd.bin.extract import extract
+    _, raw, pcms = wav_scp
+    d = tmp_path / "ssl_model"
+    d.mkdir()
+    arch = "ECAPA_TDNN_GLOB_c512"
+    sd_b = synth_state_dict(61, A.param_list(A.make_spec(arch, feat_dim=768, embed_dim=192)))
+    sd_f = synth_state_dict(62, A.hubert_params())
+    ckpt = {k: torch.from_numpy(v) for k, v in {**sd_b, **sd_f}.items()}
+    torch.save(ckpt, d / "avg_model.pt")
+    cfg = {"model": arch, "model_args": {"feat_dim": -1, "embed_dim": 192, "pooling_func": "ASTP"},
+           "dataset_args": {"frontend": "s3prl", "resample_rate": 16000, "num_frms": 150,
+                            "s3prl_args": {"upstream_args": {"name": "hubert_base"}, "download_dir": "./s3prl_hub",
+                                           "multilayer_feature": True, "layer": -1, "frozen": True,
+                                           "frame_shift": 20, "frame_length": 20},
+                            "cmvn": True, "cmvn_args": {"norm_mean": True, "norm_var": False}}}
+    with open(d / "config.yaml", "w") as f:
+        yaml.safe_dump(cfg, f)
+    scp = extract(config=str(d / "config.yaml"), model_path=str(d / "avg_model.pt"), data_type="raw",
+                  data_list=raw, embed_ark=str(tmp_path / "xv.ark"), batch_size=1, num_workers=2)
+    got = dict(load_scp_sequential(scp))
+    assert sorted(got) == sorted(pcms)
+    sdf = {k: torch.from_numpy(v) for k, v in sd_f.items()}
+    sdb = {k: torch.from_numpy(v) for k, v in sd_b.items()}
+    for k in ("u00", "u03", "u09"):
+        wav = torch.from_numpy(pcms[k][None] / 32768.0).float()
+        with torch.no_grad():
+            f = hubert_ref.s3prl_frontend(wav, sdf)
+            _, ref = models_ref.forward(arch, f - f.mean(dim=1, keepdim=True), sdb)
+        ref = ref[0].numpy()
+        assert _cos(got[k], ref) >= 0.9999
+        assert np.abs(got[k] - ref).max() < 1e-4
