@@ -1,0 +1,143 @@
+"""C5 (BASELINE.json configs[4]): the vox1-O-shaped pipeline on synthetic data —
+extract the eval set, cohort means with ONE RCCL all-reduce, cosine trials,
+AS-Norm (cohort 10k, top 300), EER / minDCF.  One process per GPU:
+
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 scripts/bench_c5.py
+
+Stages (rank-sharded where the reference shards them):
+  extract   eval utterances split contiguously over ranks (tools/extract_embedding.sh),
+            fbank + ECAPA on each rank, embeddings all-gathered (the reference
+            concatenates the per-rank scps — same bytes, done in memory here);
+  cohort    cohort utterance embeddings (synthetic, 2 per speaker) summed per
+            speaker on each rank's shard, one f64 all-reduce (dist.allreduce_sums);
+  score     cosine of every trial (wsp_cosine_pairs), AS-Norm statistics of every
+            eval utterance vs the cohort (wsp_asnorm_stats), normalised scores;
+  metrics   EER / minDCF(0.01) on rank 0 (host, as the reference).
+Prints one JSON line with per-stage seconds (max over ranks) and trials/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from wespeaker_hubert_amd import dist as wdist  # noqa: E402
+from wespeaker_hubert_amd.frontend import compute_fbank  # noqa: E402
+from wespeaker_hubert_amd.scoring import (asnorm_stats, compute_eer, compute_c_norm,  # noqa: E402
+                                          compute_pmiss_pfa_rbst, cosine_pairs, group_sums, l2_normalize)
+from wespeaker_hubert_amd.speaker_model import HipSpeakerModel  # noqa: E402
+from wespeaker_hubert_amd.synthetic import synth_audio, synth_state_dict  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--arch", default="ECAPA_TDNN_c1024")
+    ap.add_argument("--eval-utts", type=int, default=4874)
+    ap.add_argument("--seconds", type=float, default=5.0)
+    ap.add_argument("--cohort", type=int, default=10000)
+    ap.add_argument("--trials", type=int, default=37611)
+    ap.add_argument("--top-n", type=int, default=300)
+    ap.add_argument("--batch", type=int, default=256)
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+
+    D = 192
+    model = HipSpeakerModel(a.arch, feat_dim=80, embed_dim=D)
+    model.load_state_dict(synth_state_dict(1234, model.state_dict_layout()))
+    model.to(dev)
+    N = int(a.seconds * 16000)
+    lo, hi = wdist.shard_bounds(a.eval_utts, rank, world)
+    rng = np.random.default_rng(99)
+    trials_a = rng.integers(0, a.eval_utts, a.trials)
+    trials_b = rng.integers(0, a.eval_utts, a.trials)
+    labels = (rng.random(a.trials) < 0.5).astype(np.int64)
+
+    def sync():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+
+    # this rank's shard of the eval audio, resident in HBM before the clock starts
+    wavs = [torch.from_numpy(synth_audio(1000 + b0, min(a.batch, hi - b0), N)).to(dev) for b0 in range(lo, hi, a.batch)]
+    model.embed(compute_fbank(wavs[0][:2], scale=1.0, cmn=True))  # warm-up
+    n_rows = 2 * a.cohort  # cohort utterance embeddings (synthetic), this rank's shard in HBM
+    clo, chi = wdist.shard_bounds(n_rows, rank, world)
+    g = np.arange(n_rows, dtype=np.int32) // 2
+    xs = torch.from_numpy(np.random.default_rng(7).standard_normal((n_rows, D)).astype(np.float32)[clo:chi]).to(dev)
+    times = {}
+    sync()
+    t0 = time.perf_counter()
+    # ---- extract (per-rank shard, batches of a.batch)
+    mine = [model.embed(compute_fbank(w, scale=1.0, cmn=True)) for w in wavs]
+    mine = torch.cat(mine) if mine else torch.empty(0, D, device=dev)
+    if world > 1:
+        per = a.eval_utts // world + 1
+        pad = torch.zeros(per, D, device=dev)
+        pad[:mine.shape[0]] = mine
+        gathered = [torch.empty_like(pad) for _ in range(world)]
+        torch.distributed.all_gather(gathered, pad)
+        E = torch.cat([g[:wdist.shard_bounds(a.eval_utts, r, world)[1] - wdist.shard_bounds(a.eval_utts, r, world)[0]]
+                       for r, g in enumerate(gathered)])
+    else:
+        E = mine
+    sync()
+    times["extract"] = time.perf_counter() - t0
+    # ---- cohort means: 2 synthetic utterance embeddings per speaker, sharded sums + one all-reduce
+    t1 = time.perf_counter()
+    acc, cnt = group_sums(xs, g[clo:chi], a.cohort)
+    wdist.allreduce_sums(acc, cnt)
+    C = (acc / cnt.unsqueeze(1)).float()
+    sync()
+    times["cohort"] = time.perf_counter() - t1
+    # ---- scoring: mean vector, cosine trials, AS-Norm stats (top-n), normalised scores
+    t2 = time.perf_counter()
+    mean_vec = E.double().mean(0).float()
+    En = l2_normalize(E, mean_vec)
+    s = cosine_pairs(En, trials_a, trials_b)
+    mu, sd = asnorm_stats(E, C, a.top_n, mean_vec)
+    ns = 0.5 * ((s - mu[trials_a]) / sd[trials_a] + (s - mu[trials_b]) / sd[trials_b])
+    sync()
+    times["score"] = time.perf_counter() - t2
+    t3 = time.perf_counter()
+    fnr, fpr = compute_pmiss_pfa_rbst(ns, labels)
+    eer, thr = compute_eer(fnr, fpr, ns)
+    mindcf = compute_c_norm(fnr, fpr, 0.01)
+    times["metrics"] = time.perf_counter() - t3
+    total = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([total] + [times[k] for k in ("extract", "cohort", "score", "metrics")], device=dev,
+                         dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        total = float(t[0])
+        times = dict(zip(("extract", "cohort", "score", "metrics"), [float(x) for x in t[1:]]))
+    if rank == 0:
+        print(json.dumps({"metric": "vox1-O-shaped pipeline seconds (extract + cohort all-reduce + cosine + AS-Norm "
+                                    "+ EER/minDCF)", "value": round(total, 4), "unit": "s",
+                          "higher_is_better": False, "n_gpus": world,
+                          "stages_s": {k: round(v, 4) for k, v in times.items()},
+                          "trials_per_s": round(a.trials / times["score"], 1),
+                          "eval_emb_per_s": round(a.eval_utts / times["extract"], 1),
+                          "eer": float(eer), "min_dcf": float(mindcf),
+                          "config": {"arch": a.arch, "eval_utts": a.eval_utts, "seconds": a.seconds,
+                                     "cohort": a.cohort, "trials": a.trials, "top_n": a.top_n},
+                          "data": "synthetic audio / cohort embeddings / random trial labels"}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

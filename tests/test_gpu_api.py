@@ -223,3 +223,56 @@ def test_extract_driver_s3prl_hubert(wav_scp, tmp_path):
         ref = ref[0].numpy()
         assert _cos(got[k], ref) >= 0.9999
         assert np.abs(got[k] - ref).max() < 1e-4
+
+
+def _vm_worker(rank, world, port, spk2utt, scp, ark, q):
+    import torch.distributed as tdist
+    from wespeaker_hubert_amd.bin.vector_mean import compute_vector_mean
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    means = compute_vector_mean(spk2utt, scp, ark, device="cuda:0")
+    q.put((rank, means))
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_vector_mean_sharded_allreduce_world2(tmp_path):
+    """tools/vector_mean.py under torchrun: 2 ranks each sum a contiguous shard on the GPU,
+    one all-reduce combines them (gloo here: both ranks share the box's one GPU); the
+    cohort means equal the single-process ones and the f64 oracle."""
+    import socket
+    import torch.multiprocessing as mp
+    from wespeaker_hubert_amd.bin.vector_mean import compute_vector_mean
+    from wespeaker_hubert_amd.kaldi_io import WriteHelper
+    rng = np.random.default_rng(5)
+    utts = [f"utt{i:03d}" for i in range(41)]
+    embs = {u: rng.standard_normal(192).astype(np.float32) for u in utts}
+    spk = {f"spk{j}": [u for i, u in enumerate(utts) if i % 6 == j] for j in range(6)}
+    ark = str(tmp_path / "x.ark")
+    with WriteHelper(f"ark,scp:{ark},{ark[:-3]}scp") as w:
+        for u in utts:
+            w(u, embs[u])
+    s2u = str(tmp_path / "spk2utt")
+    with open(s2u, "w") as f:
+        for k, v in spk.items():
+            f.write(k + " " + " ".join(v) + "\n")
+    single = compute_vector_mean(s2u, ark[:-3] + "scp", str(tmp_path / "single.ark"))
+    ref = np.stack([np.mean(np.stack([embs[u] for u in spk[k]]).astype(np.float64), 0) for k in spk])
+    np.testing.assert_allclose(single, ref, atol=1e-6)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_vm_worker, args=(r, 2, port, s2u, ark[:-3] + "scp", str(tmp_path / "dist.ark"), q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        np.testing.assert_allclose(res[r], single, atol=1e-6)
+    got = dict(load_scp_sequential(str(tmp_path / "dist.scp")))
+    assert sorted(got) == sorted(spk)

@@ -44,6 +44,8 @@ def allreduce_sums(acc: torch.Tensor, cnt: torch.Tensor) -> Tuple[torch.Tensor, 
     if torch.distributed.get_world_size() == 1:
         return acc, cnt
     buf = torch.cat([acc.reshape(-1), cnt.reshape(-1)]).to(torch.float64)
+    if torch.distributed.get_backend() == "gloo":  # gloo reduces host tensors (CPU tests, 1-GPU rehearsal)
+        buf = buf.cpu()
     torch.distributed.all_reduce(buf, op=torch.distributed.ReduceOp.SUM)
     acc.copy_(buf[:acc.numel()].view_as(acc))
     cnt.copy_(buf[acc.numel():].view_as(cnt))
