@@ -22,7 +22,8 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from wespeaker_hubert_amd.arch import ecapa_gflop_per_utt, hubert_gflop_per_utt, make_spec  # noqa: E402
+from wespeaker_hubert_amd.arch import (RESNET_ARCHS, ecapa_gflop_per_utt, hubert_gflop_per_utt,  # noqa: E402
+                                       make_spec)
 from wespeaker_hubert_amd.frontend import compute_fbank  # noqa: E402
 from wespeaker_hubert_amd.s3prl_frontend import S3prlFrontend  # noqa: E402
 from wespeaker_hubert_amd.speaker_model import HipSpeakerModel  # noqa: E402
@@ -58,6 +59,25 @@ def profiled_traffic(symbol: str, grid: int):
             if sym.startswith(symbol) and g == str(grid) and v.get("hbm_bytes"):
                 return v["hbm_bytes"], os.path.basename(f) + ":" + sym
     return None, None
+
+
+def resnet_1x1_bytes_per_utt(arch: str, F: int, T: int, m: int = 32) -> float:
+    """Algorithmic HBM bytes of every 1x1 conv of one ResNet forward (resnet.py:72-107):
+    fp32 activations read once (+ the residual read by conv3's epilogue), output written
+    once; weights (bf16 hi+lo, L2-resident) excluded."""
+    kind, nblocks = RESNET_ARCHS[arch]
+    if kind != "bottleneck":
+        return 0.0
+    total, cin, fi, ti = 0.0, m, F, T
+    for li, n in enumerate(nblocks):
+        p = m << li
+        for bi in range(n):
+            s = 2 if (li > 0 and bi == 0) else 1
+            fo, to = (fi - 1) // s + 1, (ti - 1) // s + 1
+            total += 4.0 * fi * ti * (cin + p)             # conv1: read x, write y1
+            total += 4.0 * fo * to * (p + 4 * p + 4 * p)   # conv3: read y2 + residual, write out
+            cin, fi, ti = 4 * p, fo, to
+    return total
 
 
 def parse():
@@ -223,7 +243,17 @@ def main():
                                 "ms_per_step": round(ms / args.steps, 4),
                                 "tflops": round(fl / (avg * 1e-3) / 1e12, 2) if fl else None}
         k = kernels.get("h_fc1") if hubert else kernels.get("conv1x1_CxC")
-        if k and hubert:
+        kr = kernels.get("res_conv1x1") if args.arch.startswith("ResNet") else None
+        if kr:
+            # HBM roofline of the ResNet 1x1 convs as a class (all launches of a step)
+            byts = resnet_1x1_bytes_per_utt(args.arch, 80, T) * B
+            ach = byts / (kr["ms_per_step"] * 1e-3) / 1e9
+            roof = {"kernel": "conv_gemm_x3 ResNet 1x1 convs (res_conv1x1, all launches of a step)",
+                    "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None, "traffic_source": None,
+                    "algorithmic_bytes": byts, "launches_per_step": kr["launches_per_step"],
+                    "ms_per_step": kr["ms_per_step"]}
+        elif k and hubert:
             Th = (N - 400) // 320 + 1  # HuBERT conv frames (249 for 5 s)
             M, Nn, K = B * Th, 3072, 768
             flops = 2.0 * M * Nn * K

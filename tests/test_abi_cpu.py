@@ -31,10 +31,7 @@ def test_pure_host_entry_points():
     assert lib.wsp_fbank_num_frames(400, 400, 160) == 1
     # model creation / parameter layout is host-only until finalize()
     h = ctypes.c_void_p()
-    st = lib.wsp_model_create(b"ECAPA_TDNN_c512", 80, 192, 0, 0, ctypes.byref(h))
-    if st != 0:  # hipGetDevice without a GPU may fail: the error must be reported, not crash
-        assert lib.wsp_last_error()
-        return
+    assert lib.wsp_model_create(b"ECAPA_TDNN_c512", 80, 192, 0, 0, ctypes.byref(h)) == 0
     n = lib.wsp_model_num_params(h)
     from wespeaker_hubert_amd.arch import make_spec, param_list
     plist = param_list(make_spec("ECAPA_TDNN_c512", feat_dim=80, embed_dim=192))
@@ -49,6 +46,33 @@ def test_pure_host_entry_points():
     assert lib.wsp_model_forward(h, None, 1, 10, None, None, 0, None) != 0
     assert b"null" in lib.wsp_last_error()
     lib.wsp_model_destroy(h)
+
+
+def test_hubert_handle_layout_matches_reference_names():
+    """HuBERT_base handle (host-only until finalize): parameter names / shapes are the
+    reference checkpoint's frontend.* entries (arch.hubert_params)."""
+    from wespeaker_hubert_amd.arch import hubert_params
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.wsp_model_create(b"HuBERT_base", 1, 768, 0, 0, ctypes.byref(h)) == 0
+    try:
+        want = hubert_params()
+        assert lib.wsp_model_num_params(h) == len(want)
+        name, ndim, shape = ctypes.c_char_p(), ctypes.c_int(), (ctypes.c_int64 * 4)()
+        for i, (n, s) in enumerate(want):
+            assert lib.wsp_model_param_info(h, i, ctypes.byref(name), ctypes.byref(ndim), shape) == 0
+            assert name.value.decode() == n and tuple(shape[d] for d in range(ndim.value)) == tuple(s)
+        assert lib.wsp_model_set_option(h, b"layer", 13) != 0  # only -1..12
+        assert lib.wsp_model_set_option(h, b"layer", 6) == 0
+        t = ctypes.c_int()
+        assert lib.wsp_frontend_out_frames(h, 80000, ctypes.byref(t)) == 0 and t.value == 250
+        assert lib.wsp_frontend_out_frames(h, 399, ctypes.byref(t)) != 0
+        b = ctypes.c_size_t()
+        assert lib.wsp_frontend_workspace_bytes(h, 4, 16000, ctypes.byref(b)) == 0 and b.value > 0
+        assert lib.wsp_model_workspace_bytes(h, 4, 100, ctypes.byref(b)) != 0  # not a backbone handle
+    finally:
+        lib.wsp_model_destroy(h)
+    assert lib.wsp_model_create(b"HuBERT_base", 1, 512, 0, 0, ctypes.byref(h)) != 0
 
 
 def test_unknown_arch_is_an_error():

@@ -33,7 +33,12 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
   m.embed_dim = embed_dim;
   m.emb_bn = emb_bn;
   m.two_emb = two_emb;
-  WSP_HIP(hipGetDevice(&m.device));
+  // Creation and parameter intake are host-only; the device is bound at
+  // finalize (create's device when one was current).
+  if (hipGetDevice(&m.device) != hipSuccess) {
+    (void)hipGetLastError();
+    m.device = -1;
+  }
   if (arch == "ECAPA_TDNN_c512" || arch == "ECAPA_TDNN_GLOB_c512" || arch == "ECAPA_TDNN_c1024" ||
       arch == "ECAPA_TDNN_GLOB_c1024") {
     m.ecapa = true;
@@ -92,7 +97,8 @@ void Model::finalize() {
   WSP_CHECK(!m.finalized, "model already finalized");
   int dev = 0;
   WSP_HIP(hipGetDevice(&dev));
-  WSP_CHECK(dev == m.device, "finalize on a different device than create");
+  WSP_CHECK(m.device < 0 || dev == m.device, "finalize on a different device than create");
+  m.device = dev;
   for (auto& p : m.params)
     WSP_CHECK(p.set || p.name.find("num_batches_tracked") != std::string::npos,
               "parameter not set: " + p.name);
