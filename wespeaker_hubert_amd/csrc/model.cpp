@@ -58,6 +58,7 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
     WSP_CHECK(!two_emb, "ResNet two_emb_layer=True is not implemented");
     WSP_CHECK(feat_dim >= 8, "ResNet feat_dim must be >= 8");
     m.ecapa = false;
+    m.x3_variant = 3;  // HBM-bound 1x1 convs: two 128 x 128 blocks per CU (+4 % over variant 4)
     m.bottleneck = it->second.first;
     for (int i = 0; i < 4; ++i) m.nblocks[i] = it->second.second[i];
     m.build_resnet_params();
