@@ -77,6 +77,17 @@ int wsp_fbank(const void* wav, int wav_dtype, int B, int num_samples, int ld, fl
               float* feats, int num_bins, int sample_rate, int window_type, int cmn,
               void* stream);
 
+/* Segmented (ragged) batch of B whole utterances of different lengths in one
+ * launch — the batch_size=1 whole-utterance extraction of bin/extract.py:78-80
+ * (Dataset(whole_utt=True)) and Speaker.extract_embedding_list (speaker.py:170-179)
+ * without per-utterance launches.  Device int32 offsets: utterance b = samples
+ * [sample_offsets[b], sample_offsets[b+1]) of `wav` and frames
+ * [frame_offsets[b], frame_offsets[b+1]) of `feats` (frames_b =
+ * wsp_fbank_num_frames(samples_b, 400, 160) >= 1); max_frames = largest frames_b. */
+int wsp_fbank_segments(const void* wav, int wav_dtype, int B, const int32_t* sample_offsets,
+                       const int32_t* frame_offsets, int max_frames, float scale, float* feats,
+                       int num_bins, int sample_rate, int window_type, int cmn, void* stream);
+
 /* ------------------------------------------------------------- model --- */
 /* arch: "ECAPA_TDNN_c512", "ECAPA_TDNN_GLOB_c512", "ECAPA_TDNN_c1024",
  * "ECAPA_TDNN_GLOB_c1024", "ResNet18/34/50/101/152/221/293"
@@ -101,6 +112,16 @@ int wsp_model_workspace_bytes(const wsp_model* m, int B, int T, size_t* bytes);
  * input) -> embed [B][embed_dim] f32.  Asynchronous on `stream`. */
 int wsp_model_forward(wsp_model* m, const float* feats, int B, int T, float* embed,
                       void* workspace, size_t workspace_bytes, void* stream);
+
+/* Segmented (ragged) batch, ECAPA-TDNN handles: utterance b = rows
+ * [frame_offsets[b], frame_offsets[b+1]) of feats [total_frames][feat_dim]
+ * (device int32 offsets, frame_offsets[B] = total_frames) -> embed [B][embed_dim];
+ * each embedding equals a batch-of-one forward of that utterance
+ * (ecapa_tdnn.py:208-234 convs pad at utterance edges; pooling per utterance). */
+int wsp_model_workspace_bytes_segments(const wsp_model* m, int B, int total_frames, size_t* bytes);
+int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const int32_t* frame_offsets,
+                               int total_frames, float* embed, void* workspace, size_t workspace_bytes,
+                               void* stream);
 
 /* Runtime options (any time after create):
  *   "precision"  1 = bf16x3 split MFMA (default; fp32-class accuracy),

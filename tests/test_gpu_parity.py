@@ -209,3 +209,38 @@ def test_group_means():
     means = scoring.group_means(torch.from_numpy(x).to(DEV), g, 17)
     ref = np.stack([x[g == i].astype(np.float64).mean(0) for i in range(17)])
     np.testing.assert_allclose(means, ref, atol=1e-9)
+
+
+SEG_FRAMES = [3, 77, 498, 150, 2, 263, 41]
+
+
+@pytest.mark.parametrize("prec", [(1, 4), (1, 2), (0, 0)], ids=["bf16x3", "bf16x3_dmafallback", "f32"])
+@pytest.mark.parametrize("arch", ["ECAPA_TDNN_GLOB_c512", "ECAPA_TDNN_c1024"])
+def test_ecapa_segmented_batch_equals_batch_of_one(arch, prec):
+    """Ragged batch (wsp_model_forward_segments): utterances of 2..498 frames in one
+    launch give each utterance's batch-of-one embedding (same per-row arithmetic), and
+    the oracle's within the embedding bar."""
+    m, sd = _hip_model(arch, 17, precision=prec[0], variant=prec[1], feat_dim=80, embed_dim=192)
+    feats = [synth_feats(300 + i, 1, t, 80)[0] for i, t in enumerate(SEG_FRAMES)]
+    cat = torch.from_numpy(np.concatenate(feats)).to(DEV)
+    off = torch.tensor(np.concatenate([[0], np.cumsum(SEG_FRAMES)]), dtype=torch.int32, device=DEV)
+    got = m.embed_segments(cat, off).cpu().numpy()
+    sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
+    for i, f in enumerate(feats):
+        one = m.embed(torch.from_numpy(f[None]).to(DEV)).cpu().numpy()[0]
+        assert np.abs(got[i] - one).max() <= 1e-6, (i, np.abs(got[i] - one).max())
+        with torch.no_grad():
+            _, ref = models_ref.forward(arch, torch.from_numpy(f[None]), sdt)
+        _assert_emb(got[i:i + 1], ref.numpy())
+
+
+def test_fbank_segments_equal_per_utterance():
+    from wespeaker_hubert_amd.frontend import compute_fbank, compute_fbank_segments
+    lens = [400, 16000, 561, 48000, 12345, 80000]
+    wavs = [synth_audio(700 + i, 1, n)[0] for i, n in enumerate(lens)]
+    feats, off, frames = compute_fbank_segments([torch.from_numpy(w) for w in wavs], device=torch.device(DEV))
+    off = off.cpu().numpy()
+    assert frames == [1 + (n - 400) // 160 for n in lens] and off[-1] == feats.shape[0]
+    for i, w in enumerate(wavs):
+        one = compute_fbank(torch.from_numpy(w[None]).to(DEV), cmn=True)[0]
+        assert torch.equal(feats[off[i]:off[i + 1]], one), i

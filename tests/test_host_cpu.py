@@ -62,3 +62,16 @@ def test_s3prl_frontend_intake_and_options(caplog):
         S3prlFrontend({"name": "wavlm_large"})
     with pytest.raises(RuntimeError):
         fe.to("cpu")
+
+
+def test_ragged_pack_groups_are_contiguous_and_bounded():
+    from wespeaker_hubert_amd.batching import pack, stream_groups
+    lens = [16000, 400, 80000, 399 + 160 * 50, 48000, 1600000, 8000]
+    frames = [1 + (n - 400) // 160 for n in lens]
+    groups = pack(lens, max_frames=600)
+    assert groups[0][0] == 0 and groups[-1][1] == len(lens)
+    assert all(a[1] == b[0] for a, b in zip(groups, groups[1:]))
+    for lo, hi in groups:
+        assert hi - lo == 1 or sum(frames[lo:hi]) <= 600
+    got = list(stream_groups(((str(i), np.zeros(n)) for i, n in enumerate(lens)), 600))
+    assert [len(k) for k, _ in got] == [hi - lo for lo, hi in groups]

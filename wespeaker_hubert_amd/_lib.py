@@ -23,6 +23,8 @@ SIGNATURES = {
     "wsp_fbank_num_frames": (c_int, [c_int, c_int, c_int]),
     "wsp_fbank": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int,
                           c_int, c_int, c_void_p]),
+    "wsp_fbank_segments": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p, c_int,
+                                   c_int, c_int, c_int, c_void_p]),
     "wsp_model_create": (c_int, [c_char_p, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
     "wsp_model_destroy": (c_int, [c_void_p]),
     "wsp_model_num_params": (c_int, [c_void_p]),
@@ -35,6 +37,9 @@ SIGNATURES = {
     "wsp_model_workspace_bytes": (c_int, [c_void_p, c_int, c_int, POINTER(c_size_t)]),
     "wsp_model_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_size_t,
                                   c_void_p]),
+    "wsp_model_workspace_bytes_segments": (c_int, [c_void_p, c_int, c_int, POINTER(c_size_t)]),
+    "wsp_model_forward_segments": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                           c_size_t, c_void_p]),
     "wsp_model_set_option": (c_int, [c_void_p, c_char_p, c_int]),
     "wsp_frontend_out_frames": (c_int, [c_void_p, c_int, POINTER(c_int)]),
     "wsp_frontend_workspace_bytes": (c_int, [c_void_p, c_int, c_int, POINTER(c_size_t)]),

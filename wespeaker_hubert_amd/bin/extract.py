@@ -6,7 +6,9 @@ Same flags as the reference (fire-style; `tools/extract_embedding.sh:51-62`):
 Writes `<embed_ark>` and `<embed_ark[:-3]>scp` (extract.py:86-88).
 
 Semantics (bin/extract.py:33-120, dataset/dataset.py:136-247):
-  * batch_size == 1: whole utterances; batch_size > 1: one random chunk of
+  * batch_size == 1: whole utterances, packed into ragged (segmented) batches of
+    <= max_frames_per_batch frames (default 128000; each embedding equals the
+    utterance's batch-of-one result); batch_size > 1: one random chunk of
     ((num_frms-1)*frame_shift + frame_length)*sr/1000 samples per utterance
     (processor.get_random_chunk, repeat-padded when shorter) — seeded here
     (`--chunk_seed`, default 0) so extraction is reproducible;
@@ -38,6 +40,7 @@ import torch
 import yaml
 
 from .. import audio
+from ..batching import DEFAULT_MAX_FRAMES, embed_utterances, stream_groups
 from ..dist import shard_lines
 from ..frontend import compute_fbank
 from ..kaldi_io import WriteHelper, validate_path
@@ -186,12 +189,25 @@ def extract(config="conf/config.yaml", **kwargs):
         for k, e in zip(keys, emb):
             writer(k, e)
 
-    n = 0
-    with torch.no_grad(), WriteHelper("ark,scp:" + embed_ark + "," + embed_scp) as writer:
-        keys, wavs = [], []
-        for key, x, sr in stream:
+    def checked(items):
+        for key, x, sr in items:
             if sr != sr_target:
                 raise NotImplementedError(f"{key}: sample rate {sr} != {sr_target} (resampling not implemented)")
+            yield key, x
+
+    n = 0
+    with torch.no_grad(), WriteHelper("ark,scp:" + embed_ark + "," + embed_scp) as writer:
+        if batch_size == 1 and frontend is None:
+            # whole utterances, packed into ragged batches (each embedding = its batch-of-one result)
+            max_frames = int(configs.get("max_frames_per_batch", DEFAULT_MAX_FRAMES))
+            for keys, pcms in stream_groups(checked(stream), max_frames):
+                for k, e in zip(keys, embed_utterances(model, pcms, device, max_frames)):
+                    writer(k, e)
+                n += len(keys)
+            print(f"extracted {n} embeddings -> {embed_scp}")
+            return embed_scp
+        keys, wavs = [], []
+        for key, x in checked(stream):
             if batch_size == 1:
                 run([key], [x], writer)
             else:

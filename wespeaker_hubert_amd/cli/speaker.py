@@ -22,6 +22,7 @@ import torch
 import yaml
 
 from ..audio import load_wav
+from ..batching import embed_utterances
 from ..frontend import compute_fbank as _gpu_fbank
 from ..kaldi_io import WriteHelper
 from ..speaker_model import get_speaker_model
@@ -99,16 +100,22 @@ class Speaker:
         return outputs[0].to(torch.device('cpu'))
 
     def extract_embedding_list(self, scp_path: str) -> Tuple[List[str], List[np.ndarray]]:
-        names, embeddings = [], []
+        """speaker.py:170-179; utterances are embedded in ragged batches
+        (batching.embed_utterances: each result equals extract_embedding of that file)."""
+        names, pcms = [], []
         with open(scp_path, 'r') as read_scp:
             for line in read_scp:
                 if not line.strip():
                     continue
                 name, wav_path = line.strip().split()
+                pcm, sample_rate = load_wav(wav_path, normalize=self.wavform_norm)
+                if sample_rate != self.resample_rate:
+                    raise NotImplementedError("resampling is not implemented (16 kHz input expected)")
                 names.append(name)
-                embedding = self.extract_embedding(wav_path)
-                embeddings.append(embedding.detach().numpy())
-        return names, embeddings
+                pcms.append(pcm[0].astype(np.float32))
+        with torch.no_grad():
+            embeddings = embed_utterances(self.model, pcms, self.device)
+        return names, [np.asarray(e, dtype=np.float32) for e in embeddings]
 
     def compute_similarity(self, audio_path1: str, audio_path2: str) -> float:
         e1 = self.extract_embedding(audio_path1)

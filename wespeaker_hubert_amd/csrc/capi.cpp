@@ -85,6 +85,23 @@ int wsp_fbank(const void* wav, int wav_dtype, int B, int num_samples, int ld, fl
   });
 }
 
+int wsp_fbank_segments(const void* wav, int wav_dtype, int B, const int32_t* sample_offsets,
+                       const int32_t* frame_offsets, int max_frames, float scale, float* feats, int num_bins,
+                       int sample_rate, int window_type, int cmn, void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(num_bins == 80, "fbank: only num_mel_bins=80 is implemented");
+    WSP_CHECK(sample_rate == 16000, "fbank: only 16 kHz is implemented");
+    WSP_CHECK(window_type == WSP_WINDOW_HAMMING, "fbank: only the hamming window is implemented");
+    WSP_CHECK(wav_dtype == WSP_DTYPE_F32 || wav_dtype == WSP_DTYPE_S16, "fbank: bad dtype");
+    WSP_CHECK(B >= 0 && max_frames >= 0, "fbank: bad shape");
+    if (B > 0 && max_frames > 0) {
+      WSP_CHECK(wav && feats && sample_offsets && frame_offsets, "fbank: null pointer");
+      wsp::launch_fbank(wav, wav_dtype, B, 0, 0, scale, feats, max_frames, cmn, wsp::fbank_tables_dev(), S(stream),
+                        sample_offsets, frame_offsets);
+    }
+  });
+}
+
 int wsp_model_create(const char* arch, int feat_dim, int embed_dim, int emb_bn, int two_emb_layer,
                      wsp_model** out) {
   WSP_GUARD({
@@ -166,6 +183,22 @@ int wsp_frontend_forward(wsp_model* m, const float* wav, int B, int num_samples,
   WSP_GUARD({
     WSP_CHECK(m && wav && feats && workspace, "null argument");
     m->m.forward_frontend(wav, B, num_samples, feats, cmn, workspace, workspace_bytes, S(stream));
+  });
+}
+
+int wsp_model_workspace_bytes_segments(const wsp_model* m, int B, int total_frames, size_t* bytes) {
+  WSP_GUARD({
+    WSP_CHECK(m && bytes, "null argument");
+    *bytes = m->m.workspace_bytes_segments(B, total_frames);
+  });
+}
+
+int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const int32_t* frame_offsets,
+                               int total_frames, float* embed, void* workspace, size_t workspace_bytes,
+                               void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(m && feats && frame_offsets && embed && workspace, "null argument");
+    m->m.forward_segments(feats, B, frame_offsets, total_frames, embed, workspace, workspace_bytes, S(stream));
   });
 }
 

@@ -59,4 +59,16 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
+// Utterance of row m in a segmented (ragged) batch: seg[b] <= m < seg[b+1],
+// seg = int32 [nseg+1] row offsets (binary search; seg is tiny and cache-hot).
+__device__ __forceinline__ int seg_of(const int* __restrict__ seg, int nseg, int m) {
+  int lo = 0, hi = nseg;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (seg[mid] <= m) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
 }  // namespace wsp

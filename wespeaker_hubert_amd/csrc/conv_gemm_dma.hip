@@ -237,7 +237,7 @@ void launch_d(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipSt
 
 bool conv_gemm_dma_supported(const ConvGemmArgs& p) {
   return !p.conv2d && p.amode == kACat && p.N % 128 == 0 && (uniform_ktiles(p) || p.cseg[1] == p.cin) &&
-         p.stride <= 1 && (p.Ti == 0 || p.Ti == p.T) && !p.gcols;
+         p.stride <= 1 && (p.Ti == 0 || p.Ti == p.T) && !p.gcols && !p.seg;
 }
 
 void launch_conv_gemm_dma(const ConvGemmArgs& args, const void* whi, const void* wlo, hipStream_t s) {

@@ -35,9 +35,11 @@ constexpr int kTabWin = 0, kTabC256 = 400, kTabS256 = 656, kTabC512 = 912, kTabS
               kTabStart = 1424, kTabLen = 1504, kTabOff = 1584, kTabW = 1664;
 constexpr int kTabSize = kTabW + 1024;
 
-__global__ __launch_bounds__(256) void fbank_kernel(const void* __restrict__ wav, int dtype, int N,
+__global__ __launch_bounds__(256) void fbank_kernel(const void* __restrict__ wav, int dtype, int N_,
                                                     int ld, float scale, float* __restrict__ feats,
-                                                    int T, const float* __restrict__ tab) {
+                                                    int T_, const float* __restrict__ tab,
+                                                    const int* __restrict__ wseg,
+                                                    const int* __restrict__ fseg) {
   __shared__ __attribute__((aligned(16))) float s_tab[kTabSize];
   __shared__ float s_x[kSeg];
   __shared__ __attribute__((aligned(16))) float2 s_buf[4][2][256];
@@ -45,6 +47,13 @@ __global__ __launch_bounds__(256) void fbank_kernel(const void* __restrict__ wav
   const int b = blockIdx.x;
   const int t0 = blockIdx.y * kFPB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // uniform batch: utterance b = samples [b*ld, b*ld + N_), frames [b*T_, (b+1)*T_);
+  // segmented batch: samples [wseg[b], wseg[b+1]), frames [fseg[b], fseg[b+1])
+  const long wbase = wseg ? (long)wseg[b] : (long)b * ld;
+  const int N = wseg ? wseg[b + 1] - wseg[b] : N_;
+  const long fbase = fseg ? (long)fseg[b] : (long)b * T_;
+  const int T = fseg ? fseg[b + 1] - fseg[b] : T_;
+  if (t0 >= T) return;  // block-uniform: past this utterance's frames
 
   for (int i = tid; i < kTabSize; i += 256) s_tab[i] = tab[i];
   const long start = (long)t0 * kFS;
@@ -53,9 +62,9 @@ __global__ __launch_bounds__(256) void fbank_kernel(const void* __restrict__ wav
     float v = 0.f;
     if (i < avail) {
       if (dtype == 1)
-        v = (float)reinterpret_cast<const short*>(wav)[(long)b * ld + start + i];
+        v = (float)reinterpret_cast<const short*>(wav)[wbase + start + i];
       else
-        v = reinterpret_cast<const float*>(wav)[(long)b * ld + start + i];
+        v = reinterpret_cast<const float*>(wav)[wbase + start + i];
     }
     s_x[i] = v * scale;
   }
@@ -159,7 +168,7 @@ __global__ __launch_bounds__(256) void fbank_kernel(const void* __restrict__ wav
         float e = 0.f;
         for (int i = 0; i < n; ++i) e += bw[o + i] * pw[s0 + i];
         e = fmaxf(e, FLT_EPSILON);
-        feats[((long)b * T + t) * kNB + bin] = logf(e);
+        feats[(fbase + t) * kNB + bin] = logf(e);
       }
     }
     __syncthreads();
@@ -168,11 +177,13 @@ __global__ __launch_bounds__(256) void fbank_kernel(const void* __restrict__ wav
 
 // CMN: subtract the per-utterance mean over frames.  One workgroup per
 // utterance; 80 columns x 3 frame groups.
-__global__ __launch_bounds__(256) void cmn_kernel(float* __restrict__ feats, int T) {
+__global__ __launch_bounds__(256) void cmn_kernel(float* __restrict__ feats, int T_,
+                                                  const int* __restrict__ fseg) {
   __shared__ float part[3][kNB];
   __shared__ float mean[kNB];
   const int b = blockIdx.x, tid = threadIdx.x;
-  float* f = feats + (long)b * T * kNB;
+  const int T = fseg ? fseg[b + 1] - fseg[b] : T_;
+  float* f = feats + (fseg ? (long)fseg[b] : (long)b * T_) * kNB;
   const int c = tid % kNB, g = tid / kNB;
   if (g < 3) {
     float s = 0.f;
@@ -231,14 +242,15 @@ void fbank_tables(float* tab) {
 }
 
 void launch_fbank(const void* wav, int dtype, int B, int N, int ld, float scale, float* feats,
-                  int T, int cmn, const float* tables, hipStream_t s) {
+                  int T, int cmn, const float* tables, hipStream_t s, const int* wseg, const int* fseg) {
   if (B == 0 || T == 0) return;
-  dim3 grid(B, (T + kFPB - 1) / kFPB);
+  WSP_CHECK((wseg == nullptr) == (fseg == nullptr), "fbank: sample and frame segments go together");
+  dim3 grid(B, (T + kFPB - 1) / kFPB);  // T = frames of the longest utterance when segmented
   hipLaunchKernelGGL(fbank_kernel, grid, dim3(256), 0, s, wav, dtype, N, ld, scale, feats, T,
-                     tables);
+                     tables, wseg, fseg);
   WSP_HIP(hipGetLastError());
   if (cmn) {
-    hipLaunchKernelGGL(cmn_kernel, dim3(B), dim3(256), 0, s, feats, T);
+    hipLaunchKernelGGL(cmn_kernel, dim3(B), dim3(256), 0, s, feats, T, fseg);
     WSP_HIP(hipGetLastError());
   }
 }

@@ -41,7 +41,7 @@ struct ALoader {
   int ld0, ld1, ld2, cs1, cs2;
   int cin, dil, pad, Ti, K;
   int c4;
-  int a_r[AR], a_t[AR];  // input row / frame of tap 0 (before dil/pad)
+  int a_r[AR], a_t[AR], a_l[AR];  // input row / frame of tap 0 (before dil/pad), utterance frames
   int j, c;  // UNI: tap and channel of the current k-tile start
 
   __device__ __forceinline__ void init(const ConvGemmArgs& p, int m0, int srow, int rows_step,
@@ -65,10 +65,19 @@ struct ALoader {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int m = m0 + srow + rows_step * i;
-      const int b = m / p.T;
-      const int t = (m - b * p.T) * p.stride;
-      a_r[i] = b * p.Ti + t;
-      a_t[i] = (m < p.M) ? t : -0x40000000;  // invalid rows fail the t-range test
+      if (p.seg) {  // segmented batch (stride 1): rows are frames of utterance seg_of(m)
+        const int mm = m < p.M ? m : p.M - 1;
+        const int b = seg_of(p.seg, p.nseg, mm);
+        a_r[i] = mm;
+        a_t[i] = (m < p.M) ? mm - p.seg[b] : -0x40000000;
+        a_l[i] = p.seg[b + 1] - p.seg[b];
+      } else {
+        const int b = m / p.T;
+        const int t = (m - b * p.T) * p.stride;
+        a_r[i] = b * p.Ti + t;
+        a_t[i] = (m < p.M) ? t : -0x40000000;  // invalid rows fail the t-range test
+        a_l[i] = p.Ti;
+      }
     }
   }
 
@@ -96,7 +105,7 @@ struct ALoader {
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const int tt = a_t[i] + off;
-        const bool ok = live && tt >= 0 && tt < Ti;
+        const bool ok = live && tt >= 0 && tt < a_l[i];
         const int row = a_r[i] + off;
         ra[i] = bload4(r0, ok ? (row * ld + cl + c4) * 4 : kOOB);
         if (AMODE == kAAdd) ra[i] += bload4(r1, ok ? (row * ld1 + c + c4) * 4 : kOOB);
@@ -117,7 +126,7 @@ struct ALoader {
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const int tt = a_t[i] + off;
-        const bool ok = live && kin && tt >= 0 && tt < Ti;
+        const bool ok = live && kin && tt >= 0 && tt < a_l[i];
         const int row = a_r[i] + off;
         ra[i] = bload4(r0, ok ? (row * ld0 + cc) * 4 : kOOB);
         if (AMODE == kAAdd) ra[i] += bload4(r1, ok ? (row * ld1 + cc) * 4 : kOOB);
@@ -228,7 +237,8 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
         const int row = m0 + (wm * TM + i) * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
         float y = acc[i][j][r] + bv;
         if (p.row_bias) {
-          const int ub = (row < p.M ? row : p.M - 1) / p.T;
+          const int rowc = row < p.M ? row : p.M - 1;
+          const int ub = p.seg ? seg_of(p.seg, p.nseg, rowc) : rowc / p.T;
           y += p.row_bias[(size_t)ub * p.N + col];
         }
         if (p.act == kActRelu) y = fmaxf(y, 0.f);
@@ -254,6 +264,7 @@ inline void check_conv_args(const ConvGemmArgs& p, const char* who) {
   // buffer-load byte offsets are 32-bit: every operand must stay below 2 GiB
   // input rows: 1-D strided convs read (M / T) * Ti rows; 2-D reads B*Fi*Ti
   const long long in_rows = p.conv2d ? (long long)(p.M / (p.Fo * p.To)) * p.Fi * p.Ti
+                            : p.seg ? (long long)p.M
                                      : std::max<long long>(p.M, (long long)((p.M + p.T - 1) / p.T) * p.Ti);
   for (int i = 0; i < 3; ++i)
     WSP_CHECK(in_rows * p.lda[i] * 4 < (long long)kOOB, w + ": operand exceeds 2 GiB (split the batch)");
@@ -273,6 +284,7 @@ inline void check_conv_args(const ConvGemmArgs& p, const char* who) {
   }
   for (int i = 0; i < 3; ++i) WSP_CHECK(p.lda[i] % 4 == 0, w + ": lda must be a multiple of 4");
   if (!p.conv2d) WSP_CHECK(p.stride >= 1 && p.Ti >= 1, w + ": call normalized() first");
+  if (p.seg) WSP_CHECK(!p.conv2d && p.stride == 1 && p.Ti == p.T && p.nseg >= 1, w + ": segmented batch needs a stride-1 1-D conv");
   if (p.gcols) {
     WSP_CHECK(p.amode == kACat && p.cseg[1] == p.cin && !p.conv2d, w + ": grouped conv needs one 1-D segment");
     WSP_CHECK(p.N % p.gcols == 0 && p.gcols % 32 == 0 && p.gcin % 4 == 0, w + ": bad grouped-conv columns");

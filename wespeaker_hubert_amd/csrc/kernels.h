@@ -49,6 +49,11 @@ struct ConvGemmArgs {
   // (a block never straddles a group) and group g reads input channels
   // [g*gcin, g*gcin + cin).  gcols 0 = ungrouped.
   int gcols, gcin;
+  // Segmented (ragged) batch, 1-D stride-1 convs: utterance b owns rows
+  // [seg[b], seg[b+1]) (device int32 [nseg+1]); taps outside it read zero.
+  // null = uniform T.
+  const int* seg;
+  int nseg;
 };
 
 // Fills the 1-D defaults (stride 1, Ti = T) of a zero-initialised ConvGemmArgs.
@@ -92,20 +97,24 @@ struct SmallLinearArgs {
 };
 void launch_small_linear(const SmallLinearArgs& p, hipStream_t s);
 
-// Per-utterance statistics over frames of a channels-last buffer x [B*T][ldx]:
+// Segmented (ragged) batches: `seg` = device int32 [B+1] row offsets, utterance
+// b owning rows [seg[b], seg[b+1]); null = uniform rows b*T .. b*T + T-1.
+
+// Per-utterance statistics over frames of a channels-last buffer x [rows][ldx]:
 // mean[b][c] -> out[b*ldo + c]; if with_std: sqrt(var_unbiased + 1e-7)
 // -> out[b*ldo + std_off + c]  (pooling_layers.py TSTP / GLOB context).
 void launch_frame_stats(const float* x, int ldx, int B, int T, int C, float* out, int ldo,
-                        int with_std, int std_off, hipStream_t s);
+                        int with_std, int std_off, hipStream_t s, const int* seg = nullptr);
 
-// out[m][c] = x[m][c] + h[m][c] * g[b][c]  (SE_Res2Block residual, ecapa_tdnn.py:156)
+// out[m][c] = x[m][c] + h[m][c] * g[b][c]  (SE_Res2Block residual, ecapa_tdnn.py:156);
+// M = total rows when segmented.
 void launch_residual_scale(const float* x, const float* h, const float* g, float* out, int B,
-                           int T, int C, hipStream_t s);
+                           int T, int C, hipStream_t s, const int* seg = nullptr, int M = 0);
 
 // ASTP attentive statistics (pooling_layers.py:135-144): softmax over frames
-// of logits e [B*T][C], weighted mean/std of x [B*T][C] -> out [B][2C].
+// of logits e [rows][C], weighted mean/std of x [rows][C] -> out [B][2C].
 void launch_astp_pool(const float* e, const float* x, int B, int T, int C, float* out,
-                      hipStream_t s);
+                      hipStream_t s, const int* seg = nullptr);
 
 // ResNet stem: 1 -> C0 3x3 conv + folded BN + ReLU, (B,T,F) feats -> NHWC [B][F][T][C0].
 void launch_resnet_stem(const float* feats, int B, int T, int F, int C0, const float* w, const float* bias,
@@ -114,8 +123,11 @@ void launch_resnet_stem(const float* feats, int B, int T, int F, int C0, const f
 // Kaldi fbank + optional CMN.  `tables` = device copy of fbank_tables().
 constexpr int kFbankTableFloats = 1664 + 1024;
 void fbank_tables(float* host_tab);  // window, twiddles, sparse mel filters
+// Segmented: wseg / fseg = device int32 [B+1] sample / frame offsets, T = frames
+// of the longest utterance (grid size); N, ld unused.
 void launch_fbank(const void* wav, int dtype, int B, int N, int ld, float scale, float* feats,
-                  int T, int cmn, const float* tables, hipStream_t s);
+                  int T, int cmn, const float* tables, hipStream_t s, const int* wseg = nullptr,
+                  const int* fseg = nullptr);
 
 // HuBERT-base front end (hubert.hip).
 // conv0 (1 -> 512, k10 s5, no bias) + GroupNorm(512, 512) + GELU:

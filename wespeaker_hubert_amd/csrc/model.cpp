@@ -118,7 +118,8 @@ int Model::feat_dim() const { return impl->feat_dim; }
 
 size_t Model::workspace_bytes(int B, int T) const {
   WSP_CHECK(!impl->hubert, "HuBERT handle: use the front-end workspace query");
-  const size_t f = impl->ecapa ? impl->ecapa_ws_floats(B, T, nullptr) : impl->resnet_ws_floats(B, T, nullptr);
+  const size_t f = impl->ecapa ? impl->ecapa_ws_floats(B, (size_t)B * T, nullptr)
+                               : impl->resnet_ws_floats(B, T, nullptr);
   return f * sizeof(float) + 256;
 }
 
@@ -137,6 +138,24 @@ void Model::forward(const float* feats, int B, int T, float* embed, void* ws, si
     WSP_CHECK(m.precision == 1, "ResNet runs on the bf16x3 kernels only (precision=1)");
     m.forward_resnet(feats, B, T, embed, wsf, s);
   }
+}
+
+size_t Model::workspace_bytes_segments(int B, int M) const {
+  WSP_CHECK(impl->ecapa, "segmented batches are implemented for ECAPA-TDNN handles");
+  WSP_CHECK(B > 0 && M >= B, "segmented batch needs B >= 1 and M >= B rows");
+  return impl->ecapa_ws_floats(B, (size_t)M, nullptr) * sizeof(float) + 256;
+}
+
+void Model::forward_segments(const float* feats, int B, const int* seg, int M, float* embed, void* ws,
+                             size_t ws_bytes, hipStream_t s) {
+  Impl& m = *impl;
+  WSP_CHECK(m.ecapa, "segmented batches are implemented for ECAPA-TDNN handles");
+  WSP_CHECK(m.finalized, "forward before finalize");
+  WSP_CHECK(seg != nullptr && B > 0 && M >= B, "segmented batch needs offsets, B >= 1 and M >= B rows");
+  WSP_CHECK((size_t)M * 1536 < (1u << 31) / 4, "segmented batch too large");
+  WSP_CHECK(ws_bytes >= workspace_bytes_segments(B, M), "workspace too small");
+  float* wsf = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+  m.forward_ecapa(feats, B, 1, embed, wsf, s, seg, M);  // T unused when segmented
 }
 
 void Model::profile(bool on) { impl->prof = on; }

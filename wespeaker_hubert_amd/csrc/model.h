@@ -28,6 +28,11 @@ class Model {
   size_t frontend_workspace_bytes(int B, int N) const;
   void forward_frontend(const float* wav, int B, int N, float* feats, int cmn, void* ws, size_t ws_bytes,
                         hipStream_t s);
+  // Segmented (ragged) batch: utterance b = feats rows [seg[b], seg[b+1]) (device int32
+  // [B+1]), M = seg[B] rows in total.  ECAPA-TDNN only.
+  size_t workspace_bytes_segments(int B, int M) const;
+  void forward_segments(const float* feats, int B, const int* seg, int M, float* embed, void* ws, size_t ws_bytes,
+                        hipStream_t s);
   void profile(bool on);
   void set_option(const std::string& key, int value);
   void profile_query(const std::string& tag, int* launches, double* total_ms, double* flops);

@@ -159,6 +159,10 @@ struct Model::Impl {
   size_t hubert_ws_floats(int B, int N, size_t* offs) const;
   void forward_hubert(const float* wav, int B, int N, float* feats, int cmn, float* ws, hipStream_t s);
 
+  // segmented (ragged) forward in progress: device row offsets [cur_nseg + 1]
+  const int* cur_seg = nullptr;
+  int cur_nseg = 0;
+
   // 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA
   int precision = 1;
   int x3_variant = 4;  // 256 x 128 swizzled-LDS bf16x3 tiles (tools/gemm_bench: +3-8 % over 1)
@@ -625,10 +629,12 @@ struct Model::Impl {
     g.out = out;
     g.ldo = ldo;
     g.act = act;
+    g.seg = cur_seg;
+    g.nseg = cur_nseg;
   }
 
-  size_t ecapa_ws_floats(int B, int T, size_t* offs) const {
-    const size_t M = (size_t)B * T;
+  // M = frame rows of the batch (B * T, or the segment total)
+  size_t ecapa_ws_floats(int B, size_t M, size_t* offs) const {
     const size_t sizes[] = {M * C, M * C, M * C, M * C,           // x1..x4
                             M * C, M * C, M * C,                   // h1..h3
                             (size_t)B * C, (size_t)B * 128, (size_t)B * C,  // gmean, ghid, gate
@@ -642,10 +648,15 @@ struct Model::Impl {
     return o;
   }
 
-  void forward_ecapa(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
-    const int M = B * T, w = C / 8;
+  // seg (device [B+1] row offsets) non-null: ragged batch of M rows; T unused by the
+  // kernels then (per-utterance lengths come from seg).
+  void forward_ecapa(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s,
+                     const int* seg = nullptr, int M_seg = 0) {
+    const int M = seg ? M_seg : B * T, w = C / 8;
+    cur_seg = seg;
+    cur_nseg = B;
     size_t off[16];
-    ecapa_ws_floats(B, T, off);
+    ecapa_ws_floats(B, M, off);
     float* x[5] = {nullptr, ws + off[0], ws + off[1], ws + off[2], ws + off[3]};
     float* h1 = ws + off[4];
     float* h2 = ws + off[5];
@@ -699,10 +710,10 @@ struct Model::Impl {
         run("conv1x1_CxC", 2.0 * M * C * C, s, [&] { launch(g, b.c3, s); });
       }
       run("se", 0, s, [&] {
-        launch_frame_stats(h3, C, B, T, C, gmean, C, 0, 0, s);
+        launch_frame_stats(h3, C, B, T, C, gmean, C, 0, 0, s, seg);
         launch_small_linear({gmean, C, b.se1.wt, b.se1.bias, ghid, 128, B, C, 128, 1}, s);
         launch_small_linear({ghid, 128, b.se2.wt, b.se2.bias, gate, C, B, 128, C, 3}, s);
-        launch_residual_scale(xin, h3, gate, x[li + 2], B, T, C, s);
+        launch_residual_scale(xin, h3, gate, x[li + 2], B, T, C, s, seg, M);
       });
     }
     {
@@ -721,7 +732,7 @@ struct Model::Impl {
     }
     if (glob) {
       run("glob_ctx", 0, s, [&] {
-        launch_frame_stats(xp, 1536, B, T, 1536, gstats, 3072, 1, 1536, s);
+        launch_frame_stats(xp, 1536, B, T, 1536, gstats, 3072, 1, 1536, s, seg);
         launch_small_linear({gstats, 3072, pool1_ctx.wt, pool1_ctx.bias, rowb, 128, B, 3072, 128, 0}, s);
       });
       gemm("pool_linear1", pool1, xp, 1536, att, 128, M, T, 1, 0, kActTanh, s, rowb, false);
@@ -729,10 +740,12 @@ struct Model::Impl {
       gemm("pool_linear1", pool1, xp, 1536, att, 128, M, T, 1, 0, kActTanh, s);
     }
     gemm("pool_linear2", pool2, att, 128, logit, 1536, M, T, 1, 0, kActNone, s);
-    run("astp", 0, s, [&] { launch_astp_pool(logit, xp, B, T, 1536, pooled, s); });
+    run("astp", 0, s, [&] { launch_astp_pool(logit, xp, B, T, 1536, pooled, s, seg); });
     run("head", 0, s, [&] {
       launch_small_linear({pooled, 3072, head.wt, head.bias, embed, embed_dim, B, 3072, embed_dim, 0}, s);
     });
+    cur_seg = nullptr;
+    cur_nseg = 0;
   }
 };
 

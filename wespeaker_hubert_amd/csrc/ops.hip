@@ -81,15 +81,17 @@ void launch_small_linear(const SmallLinearArgs& p, hipStream_t s) {
 // variance (torch.var default, pooling_layers.py:81,131).
 namespace {
 __global__ __launch_bounds__(256) void frame_stats_kernel(const float* __restrict__ x, int ldx,
-                                                          int T, int C, float* __restrict__ out,
-                                                          int ldo, int with_std, int std_off) {
+                                                          int T_, int C, float* __restrict__ out,
+                                                          int ldo, int with_std, int std_off,
+                                                          const int* __restrict__ seg) {
   __shared__ float part[4][64];
   __shared__ float s_mean[64];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = blockIdx.y * 64 + lane;
   const bool ok = c < C;
-  const float* xb = x + (long)b * T * ldx + c;
+  const int T = seg ? seg[b + 1] - seg[b] : T_;
+  const float* xb = x + (seg ? (long)seg[b] : (long)b * T_) * ldx + c;
   float s = 0.f;
   if (ok)
     for (int t = wave; t < T; t += 4) s += xb[(long)t * ldx];
@@ -120,11 +122,11 @@ __global__ __launch_bounds__(256) void frame_stats_kernel(const float* __restric
 }  // namespace
 
 void launch_frame_stats(const float* x, int ldx, int B, int T, int C, float* out, int ldo,
-                        int with_std, int std_off, hipStream_t s) {
+                        int with_std, int std_off, hipStream_t s, const int* seg) {
   if (B == 0) return;
   dim3 grid(B, ceil_div(C, 64));
   hipLaunchKernelGGL(frame_stats_kernel, grid, dim3(256), 0, s, x, ldx, T, C, out, ldo, with_std,
-                     std_off);
+                     std_off, seg);
   WSP_HIP(hipGetLastError());
 }
 
@@ -134,11 +136,12 @@ __global__ __launch_bounds__(256) void residual_scale_kernel(const f32x4* __rest
                                                              const f32x4* __restrict__ h,
                                                              const float* __restrict__ g,
                                                              f32x4* __restrict__ out, long n4,
-                                                             int T, int C4) {
+                                                             int T, int C4, const int* __restrict__ seg,
+                                                             int nseg) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     const long row = i / C4;
     const int c4 = (int)(i - row * C4);
-    const int b = (int)(row / T);
+    const int b = seg ? seg_of(seg, nseg, (int)row) : (int)(row / T);
     const f32x4 gv = *reinterpret_cast<const f32x4*>(g + ((long)b * C4 + c4) * 4);
     out[i] = x[i] + h[i] * gv;
   }
@@ -146,14 +149,14 @@ __global__ __launch_bounds__(256) void residual_scale_kernel(const f32x4* __rest
 }  // namespace
 
 void launch_residual_scale(const float* x, const float* h, const float* g, float* out, int B,
-                           int T, int C, hipStream_t s) {
+                           int T, int C, hipStream_t s, const int* seg, int M) {
   WSP_CHECK(C % 4 == 0, "residual_scale: C % 4");
-  const long n4 = (long)B * T * C / 4;
+  const long n4 = (long)(seg ? M : B * T) * C / 4;
   if (n4 == 0) return;
   const int grid = (int)std::min<long>(ceil_div((int)std::min<long>(n4, 1L << 30), 256), 256 * 16);
   hipLaunchKernelGGL(residual_scale_kernel, dim3(grid), dim3(256), 0, s,
                      reinterpret_cast<const f32x4*>(x), reinterpret_cast<const f32x4*>(h), g,
-                     reinterpret_cast<f32x4*>(out), n4, T, C / 4);
+                     reinterpret_cast<f32x4*>(out), n4, T, C / 4, seg, B);
   WSP_HIP(hipGetLastError());
 }
 
@@ -162,16 +165,17 @@ void launch_residual_scale(const float* x, const float* h, const float* g, float
 // first and second moments: one read of logits and features, no alpha tensor.
 namespace {
 __global__ __launch_bounds__(256) void astp_pool_kernel(const float* __restrict__ e,
-                                                        const float* __restrict__ x, int T, int C,
-                                                        float* __restrict__ out) {
+                                                        const float* __restrict__ x, int T_, int C,
+                                                        float* __restrict__ out, const int* __restrict__ seg) {
   __shared__ float sm[4][4][64];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = blockIdx.y * 64 + lane;
   const bool ok = c < C;
   float mx = -INFINITY, se = 0.f, a1 = 0.f, a2 = 0.f;
+  const int T = seg ? seg[b + 1] - seg[b] : T_;
   if (ok) {
-    const long base = (long)b * T * C + c;
+    const long base = (seg ? (long)seg[b] : (long)b * T_) * C + c;
     for (int t = wave; t < T; t += 4) {
       const float ev = e[base + (long)t * C];
       const float xv = x[base + (long)t * C];
@@ -214,10 +218,10 @@ __global__ __launch_bounds__(256) void astp_pool_kernel(const float* __restrict_
 }  // namespace
 
 void launch_astp_pool(const float* e, const float* x, int B, int T, int C, float* out,
-                      hipStream_t s) {
+                      hipStream_t s, const int* seg) {
   if (B == 0) return;
   dim3 grid(B, ceil_div(C, 64));
-  hipLaunchKernelGGL(astp_pool_kernel, grid, dim3(256), 0, s, e, x, T, C, out);
+  hipLaunchKernelGGL(astp_pool_kernel, grid, dim3(256), 0, s, e, x, T, C, out, seg);
   WSP_HIP(hipGetLastError());
 }
 

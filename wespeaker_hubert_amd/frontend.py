@@ -7,6 +7,8 @@ extraction, bin/extract.py:66-67).
 """
 from __future__ import annotations
 
+import itertools
+
 import torch
 
 from . import _lib
@@ -45,3 +47,29 @@ def compute_fbank(wav: torch.Tensor, scale: float = 1.0, cmn: bool = True, num_m
                                      num_mel_bins, sample_rate, _lib.WSP_WINDOW_HAMMING, int(cmn), stream),
                "wsp_fbank")
     return out
+
+
+def compute_fbank_segments(wavs, scale: float = 1.0, cmn: bool = True, device=None):
+    """Whole utterances of different lengths in one launch (wsp_fbank_segments).
+
+    `wavs`: sequence of 1-D arrays / tensors (int16-valued float or int16), each >= 400
+    samples.  Returns (feats [sum T_b][80] float32 on the device, frame_offsets int32
+    [B+1] on the device, frame counts list).  Row block b equals
+    compute_fbank(wavs[b])[0] exactly."""
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    lens = [int(len(w)) for w in wavs]
+    if any(n < FRAME_LEN for n in lens):
+        raise ValueError("every utterance needs >= 400 samples (one 25 ms frame)")
+    frames = [num_frames(n) for n in lens]
+    cat = torch.cat([torch.as_tensor(w).reshape(-1).to(torch.float32) for w in wavs]).to(device)
+    so = torch.tensor([0] + list(itertools.accumulate(lens)), dtype=torch.int32, device=device)
+    fo_host = [0] + list(itertools.accumulate(frames))
+    fo = torch.tensor(fo_host, dtype=torch.int32, device=device)
+    feats = torch.empty(fo_host[-1], NUM_BINS, dtype=torch.float32, device=device)
+    stream = torch.cuda.current_stream(device).cuda_stream
+    _lib.check(_lib.load().wsp_fbank_segments(cat.data_ptr(), _lib.WSP_DTYPE_F32, len(lens), so.data_ptr(),
+                                              fo.data_ptr(), max(frames), float(scale), feats.data_ptr(),
+                                              NUM_BINS, 16000, _lib.WSP_WINDOW_HAMMING, int(cmn), stream),
+               "wsp_fbank_segments")
+    return feats, fo, frames

@@ -217,6 +217,36 @@ class HipSpeakerModel(_HipHandle):
                                                  ws.data_ptr(), ws.numel(), stream), "wsp_model_forward")
         return out
 
+    def embed_segments(self, feats: torch.Tensor, frame_offsets: torch.Tensor,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Ragged batch (ECAPA-TDNN): utterance b = rows [off[b], off[b+1]) of feats
+        [sum T_b][feat_dim]; frame_offsets = int32 [B+1] on the same device.  Each row of
+        the result equals embed(feats_b[None])."""
+        if not feats.is_cuda or not frame_offsets.is_cuda:
+            raise RuntimeError("feats / frame_offsets must be HIP device tensors")
+        if self._handle is None or self._device != feats.device.index:
+            self.to(feats.device)
+        if feats.dim() != 2 or feats.shape[1] != self.spec.feat_dim:
+            raise ValueError(f"expected (rows, {self.spec.feat_dim}) features, got {tuple(feats.shape)}")
+        feats = feats.float().contiguous()
+        off = frame_offsets.to(torch.int32).contiguous()
+        B, M = off.numel() - 1, feats.shape[0]
+        if out is None:
+            out = torch.empty(B, self.spec.embed_dim, dtype=torch.float32, device=feats.device)
+        b = ctypes.c_size_t()
+        _lib.check(_lib.load().wsp_model_workspace_bytes_segments(self._handle, B, M, ctypes.byref(b)),
+                   "workspace_bytes_segments")
+        ws = self._workspace_tensor(b.value, feats.device)
+        stream = torch.cuda.current_stream(feats.device).cuda_stream
+        _lib.check(_lib.load().wsp_model_forward_segments(self._handle, feats.data_ptr(), B, off.data_ptr(), M,
+                                                          out.data_ptr(), ws.data_ptr(), ws.numel(), stream),
+                   "wsp_model_forward_segments")
+        return out
+
+    @property
+    def supports_segments(self) -> bool:
+        return self.spec.family == "ecapa"
+
     def __call__(self, feats: torch.Tensor):
         return None, self.embed(feats)
 
