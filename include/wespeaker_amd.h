@@ -137,7 +137,7 @@ int wsp_model_set_option(wsp_model* m, const char* key, int value);
  * around every launch (used by bench.py for the roofline figure). */
 int wsp_model_profile(wsp_model* m, int enable);
 /* Synchronises the events; returns launches, summed ms and algorithmic
- * FLOPs per launch of the named kernel class, then clears it. */
+ * FLOPs per launch (mean over the launches) of the named kernel class, then clears it. */
 int wsp_model_profile_query(wsp_model* m, const char* kernel_class, int* launches,
                             double* total_ms, double* flops_per_launch);
 
@@ -156,6 +156,17 @@ int wsp_frontend_workspace_bytes(const wsp_model* m, int B, int num_samples, siz
  * -> feats [B][frames][768] f32.  Asynchronous on `stream`. */
 int wsp_frontend_forward(wsp_model* m, const float* wav, int B, int num_samples, float* feats, int cmn,
                          void* workspace, size_t workspace_bytes, void* stream);
+
+/* Ragged batch: B whole utterances concatenated in `wav` (device), utterance b =
+ * num_samples[b] samples (HOST int32 array, each >= 400) -> feats rows
+ * [frame_offsets[b], frame_offsets[b+1]) of [sum_b ceil(num_samples[b]/320)][768]
+ * (frame_offsets: HOST int32 [B+1] output, may be NULL).  Each utterance's rows
+ * equal its batch-of-one result (conv padding, attention, length match, CMN per
+ * utterance). */
+int wsp_frontend_workspace_bytes_segments(const wsp_model* m, int B, const int32_t* num_samples, size_t* bytes);
+int wsp_frontend_forward_segments(wsp_model* m, const float* wav, int B, const int32_t* num_samples, float* feats,
+                                  int32_t* frame_offsets, int cmn, void* workspace, size_t workspace_bytes,
+                                  void* stream);
 
 /* ------------------------------------------------------------ scoring --- */
 /* y[r] = x[r] - sub (sub may be NULL), then L2-normalised; [R][D] f32. */

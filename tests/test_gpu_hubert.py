@@ -124,3 +124,27 @@ def test_hubert_ecapa_chain_embeddings(sd_np, sd_t):
     cos = (got * ref).sum(1) / (np.linalg.norm(got, axis=1) * np.linalg.norm(ref, axis=1))
     assert d < EMB_ATOL, f"max |delta| {d}"
     assert cos.min() >= EMB_COS
+
+
+@pytest.mark.parametrize("layer,multi", [(-1, True), (3, False)])
+def test_ragged_batch_equals_batch_of_one(sd_np, sd_t, layer, multi):
+    """wsp_frontend_forward_segments: utterances of different lengths in one launch
+    give each utterance's batch-of-one features (and the oracle's)."""
+    lens = [400, 12345, 16000, 8007, 48000, 1999]
+    wavs = [_wav(40 + i, 1, n)[0] for i, n in enumerate(lens)]
+    fe = _frontend(sd_np, layer=layer, multilayer=multi)
+    feats, offs = fe.extract_segments([torch.from_numpy(w) for w in wavs], cmn=True)
+    assert offs == list(np.concatenate([[0], np.cumsum([s3prl_num_frames(n) for n in lens])]))
+    for i, w in enumerate(wavs):
+        one = fe.extract(torch.from_numpy(w[None]).to(DEV), cmn=True)[0]
+        got = feats[offs[i]:offs[i + 1]]
+        assert (got - one).abs().max().item() <= 1e-5, i
+        if i in (0, 3):
+            with torch.no_grad():
+                if layer < 0:
+                    ref = hubert_ref.s3prl_frontend(torch.from_numpy(w[None]), sd_t)
+                else:
+                    ref = hubert_ref.match_length(hubert_ref.hubert_hidden_states(torch.from_numpy(w[None]), sd_t)[layer],
+                                                  len(w))
+            ref = _cmn(ref)[0]
+            assert (got.cpu() - ref).abs().max().item() <= FEAT_ATOL

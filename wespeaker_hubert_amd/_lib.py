@@ -45,6 +45,9 @@ SIGNATURES = {
     "wsp_frontend_workspace_bytes": (c_int, [c_void_p, c_int, c_int, POINTER(c_size_t)]),
     "wsp_frontend_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_size_t,
                                      c_void_p]),
+    "wsp_frontend_workspace_bytes_segments": (c_int, [c_void_p, c_int, c_void_p, POINTER(c_size_t)]),
+    "wsp_frontend_forward_segments": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                              c_void_p, c_size_t, c_void_p]),
     "wsp_model_profile": (c_int, [c_void_p, c_int]),
     "wsp_model_profile_query": (c_int, [c_void_p, c_char_p, POINTER(c_int), POINTER(c_double),
                                         POINTER(c_double)]),

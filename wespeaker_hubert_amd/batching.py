@@ -39,10 +39,33 @@ def pack(lengths: Sequence[int], max_frames: int = DEFAULT_MAX_FRAMES) -> List[T
     return groups
 
 
+def _pack_samples(lengths: Sequence[int], budget: int) -> List[Tuple[int, int]]:
+    groups, lo, acc = [], 0, 0
+    for i, n in enumerate(lengths):
+        if i > lo and acc + n > budget:
+            groups.append((lo, i))
+            lo, acc = i, 0
+        acc += n
+    if lo < len(lengths):
+        groups.append((lo, len(lengths)))
+    return groups
+
+
 def embed_utterances(model, pcms: Sequence, device, max_frames: int = DEFAULT_MAX_FRAMES,
-                     scale: float = 1.0) -> List[np.ndarray]:
-    """Embeddings of whole utterances (int16-valued PCM), in input order."""
+                     scale: float = 1.0, frontend=None) -> List[np.ndarray]:
+    """Embeddings of whole utterances (int16-valued PCM), in input order.  With an SSL
+    `frontend` (S3prlFrontend) the audio is fed as [-1, 1] floats (x / 32768, as
+    torchaudio.load(normalize=True)), then CMN, then the backbone — all ragged."""
     out: List[np.ndarray] = []
+    if frontend is not None:
+        budget = max(1, max_frames) * 160  # samples per group, ~ the fbank-frame budget in audio time
+        for lo, hi in _pack_samples([len(x) for x in pcms], budget):
+            wav = [torch.from_numpy(np.asarray(x, np.float32) * (1.0 / 32768.0)) for x in pcms[lo:hi]]
+            feats, offs = frontend.extract_segments(wav, cmn=True)
+            off = torch.tensor(offs, dtype=torch.int32, device=feats.device)
+            emb = model.embed_segments(feats, off).cpu().numpy()
+            out.extend(emb[i] for i in range(hi - lo))
+        return out
     if not getattr(model, "supports_segments", False):
         for x in pcms:  # ResNet: per-utterance forward
             feats = compute_fbank(torch.as_tensor(np.asarray(x, np.float32)).to(device)[None], scale=scale, cmn=True)

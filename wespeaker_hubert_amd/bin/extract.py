@@ -197,11 +197,11 @@ def extract(config="conf/config.yaml", **kwargs):
 
     n = 0
     with torch.no_grad(), WriteHelper("ark,scp:" + embed_ark + "," + embed_scp) as writer:
-        if batch_size == 1 and frontend is None:
+        if batch_size == 1:
             # whole utterances, packed into ragged batches (each embedding = its batch-of-one result)
             max_frames = int(configs.get("max_frames_per_batch", DEFAULT_MAX_FRAMES))
             for keys, pcms in stream_groups(checked(stream), max_frames):
-                for k, e in zip(keys, embed_utterances(model, pcms, device, max_frames)):
+                for k, e in zip(keys, embed_utterances(model, pcms, device, max_frames, frontend=frontend)):
                     writer(k, e)
                 n += len(keys)
             print(f"extracted {n} embeddings -> {embed_scp}")

@@ -202,6 +202,23 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
   });
 }
 
+int wsp_frontend_workspace_bytes_segments(const wsp_model* m, int B, const int32_t* num_samples, size_t* bytes) {
+  WSP_GUARD({
+    WSP_CHECK(m && num_samples && bytes, "null argument");
+    *bytes = m->m.frontend_workspace_bytes_segments(B, num_samples);
+  });
+}
+
+int wsp_frontend_forward_segments(wsp_model* m, const float* wav, int B, const int32_t* num_samples, float* feats,
+                                  int32_t* frame_offsets, int cmn, void* workspace, size_t workspace_bytes,
+                                  void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(m && wav && num_samples && feats && workspace, "null argument");
+    m->m.forward_frontend_segments(wav, B, num_samples, feats, frame_offsets, cmn, workspace, workspace_bytes,
+                                   S(stream));
+  });
+}
+
 int wsp_model_set_option(wsp_model* m, const char* key, int value) {
   WSP_GUARD({
     WSP_CHECK(m && key, "null argument");

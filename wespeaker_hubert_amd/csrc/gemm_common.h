@@ -65,12 +65,14 @@ struct ALoader {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int m = m0 + srow + rows_step * i;
-      if (p.seg) {  // segmented batch (stride 1): rows are frames of utterance seg_of(m)
+      if (p.seg) {  // segmented batch: output row m = frame t of utterance seg_of(m)
         const int mm = m < p.M ? m : p.M - 1;
         const int b = seg_of(p.seg, p.nseg, mm);
-        a_r[i] = mm;
-        a_t[i] = (m < p.M) ? mm - p.seg[b] : -0x40000000;
-        a_l[i] = p.seg[b + 1] - p.seg[b];
+        const int t = (mm - p.seg[b]) * p.stride;
+        const int* is = p.iseg ? p.iseg : p.seg;
+        a_r[i] = is[b] + t;
+        a_t[i] = (m < p.M) ? t : -0x40000000;
+        a_l[i] = is[b + 1] - is[b];
       } else {
         const int b = m / p.T;
         const int t = (m - b * p.T) * p.stride;
@@ -264,7 +266,7 @@ inline void check_conv_args(const ConvGemmArgs& p, const char* who) {
   // buffer-load byte offsets are 32-bit: every operand must stay below 2 GiB
   // input rows: 1-D strided convs read (M / T) * Ti rows; 2-D reads B*Fi*Ti
   const long long in_rows = p.conv2d ? (long long)(p.M / (p.Fo * p.To)) * p.Fi * p.Ti
-                            : p.seg ? (long long)p.M
+                            : p.seg ? (long long)std::max(p.M, p.Ti)
                                      : std::max<long long>(p.M, (long long)((p.M + p.T - 1) / p.T) * p.Ti);
   for (int i = 0; i < 3; ++i)
     WSP_CHECK(in_rows * p.lda[i] * 4 < (long long)kOOB, w + ": operand exceeds 2 GiB (split the batch)");
@@ -284,7 +286,7 @@ inline void check_conv_args(const ConvGemmArgs& p, const char* who) {
   }
   for (int i = 0; i < 3; ++i) WSP_CHECK(p.lda[i] % 4 == 0, w + ": lda must be a multiple of 4");
   if (!p.conv2d) WSP_CHECK(p.stride >= 1 && p.Ti >= 1, w + ": call normalized() first");
-  if (p.seg) WSP_CHECK(!p.conv2d && p.stride == 1 && p.Ti == p.T && p.nseg >= 1, w + ": segmented batch needs a stride-1 1-D conv");
+  if (p.seg) WSP_CHECK(!p.conv2d && p.nseg >= 1 && (p.iseg || p.stride == 1), w + ": segmented batch needs a 1-D conv (input offsets when strided)");
   if (p.gcols) {
     WSP_CHECK(p.amode == kACat && p.cseg[1] == p.cin && !p.conv2d, w + ": grouped conv needs one 1-D segment");
     WSP_CHECK(p.N % p.gcols == 0 && p.gcols % 32 == 0 && p.gcin % 4 == 0, w + ": bad grouped-conv columns");

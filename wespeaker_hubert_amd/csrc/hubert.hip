@@ -28,17 +28,24 @@ constexpr int kC0 = 512, kK0 = 10, kS0 = 5, kTC = 128;
 // PASS 2: out = GELU(GroupNorm(y)).  One thread per channel, one block per
 // (128-frame chunk, utterance); the waveform chunk is staged in LDS and read
 // as a broadcast.
+// Segmented batch (wseg / oseg non-null): utterance b = samples [wseg[b], wseg[b+1])
+// -> output rows [oseg[b], oseg[b+1]); GroupNorm statistics per utterance as before.
 template <int PASS>
-__global__ __launch_bounds__(kC0) void conv0_kernel(const float* __restrict__ wav, int N, int ldw, int T0,
+__global__ __launch_bounds__(kC0) void conv0_kernel(const float* __restrict__ wav, int N_, int ldw, int T0_,
                                                     const float* __restrict__ w, const float* __restrict__ gamma,
                                                     const float* __restrict__ beta, double* __restrict__ stats,
-                                                    float* __restrict__ out, int B) {
-  __shared__ float seg[kTC * kS0 + kK0];
+                                                    float* __restrict__ out, int B, const int* __restrict__ wseg,
+                                                    const int* __restrict__ oseg) {
+  __shared__ float xs[kTC * kS0 + kK0];
   const int b = blockIdx.y, t0 = blockIdx.x * kTC, c = threadIdx.x;
-  const float* x = wav + (size_t)b * ldw;
+  const int N = wseg ? wseg[b + 1] - wseg[b] : N_;
+  const int T0 = oseg ? oseg[b + 1] - oseg[b] : T0_;
+  if (t0 >= T0) return;  // block-uniform: past this utterance
+  const float* x = wav + (wseg ? (size_t)wseg[b] : (size_t)b * ldw);
+  const size_t obase = oseg ? (size_t)oseg[b] : (size_t)b * T0_;
   for (int i = c; i < kTC * kS0 + kK0; i += kC0) {
     const int n = t0 * kS0 + i;
-    seg[i] = n < N ? x[n] : 0.f;
+    xs[i] = n < N ? x[n] : 0.f;
   }
   float wr[kK0];
 #pragma unroll
@@ -58,14 +65,14 @@ __global__ __launch_bounds__(kC0) void conv0_kernel(const float* __restrict__ wa
   for (int t = 0; t < nt; ++t) {
     float y = 0.f;
 #pragma unroll
-    for (int k = 0; k < kK0; ++k) y = fmaf(wr[k], seg[t * kS0 + k], y);
+    for (int k = 0; k < kK0; ++k) y = fmaf(wr[k], xs[t * kS0 + k], y);
     if (PASS == 0) {
       acc += y;
     } else if (PASS == 1) {
       const float d = y - mean;
       acc = fmaf(d, d, acc);
     } else {
-      out[((size_t)b * T0 + t0 + t) * kC0 + c] = gelu_erf(fmaf(y, scale, shift));
+      out[(obase + t0 + t) * kC0 + c] = gelu_erf(fmaf(y, scale, shift));
     }
   }
   if (PASS == 0) atomicAdd(s0, (double)acc);
@@ -112,11 +119,25 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LayerNormArgs p) {
   }
   if (p.feat) {
     // s3prl Featurizer: feat += w_l * h_l; length match replicates the last
-    // frame up to Tout (and trims frames >= Tout).
-    const int b = row / p.T, t = row - b * p.T;
-    const int t_end = (t == p.T - 1) ? p.Tout : min(t + 1, p.Tout);
+    // frame up to Tout (and trims frames >= Tout).  Segmented: per utterance.
+    int b, t, T, Tout;
+    size_t fbase;
+    if (p.seg) {
+      b = seg_of(p.seg, p.nseg, row);
+      t = row - p.seg[b];
+      T = p.seg[b + 1] - p.seg[b];
+      Tout = p.fseg[b + 1] - p.fseg[b];
+      fbase = p.fseg[b];
+    } else {
+      b = row / p.T;
+      t = row - b * p.T;
+      T = p.T;
+      Tout = p.Tout;
+      fbase = (size_t)b * p.Tout;
+    }
+    const int t_end = (t == T - 1) ? Tout : min(t + 1, Tout);
     for (int tt = t; tt < t_end; ++tt) {
-      float* f = p.feat + ((size_t)b * p.Tout + tt) * D;
+      float* f = p.feat + (fbase + tt) * D;
 #pragma unroll
       for (int i = 0; i < VPL; ++i) {
         const int c = lane + 64 * i;
@@ -162,13 +183,17 @@ __device__ __forceinline__ f32x16 mma3(const bf16x8& ah, const bf16x8& al, const
 }
 
 __global__ __launch_bounds__(256) void mha_kernel(const float* __restrict__ qkv, int ldq, float* __restrict__ out,
-                                                  int ldo, int T, int D, float scale) {
+                                                  int ldo, int T_, int D, float scale, const int* __restrict__ seg) {
   __shared__ __attribute__((aligned(16))) float Ks[2][kKC * kKLD];
   __shared__ __attribute__((aligned(16))) float VTs[2][kDH * kVLD];
   const int b = blockIdx.z, head = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int q = blockIdx.x * (kQW * kWaves) + wave * kQW + r;
-  const float* base = qkv + (size_t)b * T * ldq;
+  // segmented batch: utterance b = rows [seg[b], seg[b+1]); attention stays inside it
+  const size_t rbase = seg ? (size_t)seg[b] : (size_t)b * T_;
+  const int T = seg ? seg[b + 1] - seg[b] : T_;
+  if (blockIdx.x * (kQW * kWaves) >= T) return;  // block-uniform
+  const float* base = qkv + rbase * ldq;
   const float* kbase = base + D + head * kDH;
   const float* vbase = base + 2 * D + head * kDH;
 
@@ -279,7 +304,7 @@ __global__ __launch_bounds__(256) void mha_kernel(const float* __restrict__ qkv,
   }
   const float inv = 1.f / (l + __shfl_xor(l, 32, 64));
   if (q < T) {
-    float* op = out + ((size_t)b * T + q) * ldo + head * kDH + 4 * hh;
+    float* op = out + (rbase + q) * ldo + head * kDH + 4 * hh;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -293,10 +318,12 @@ __global__ __launch_bounds__(256) void mha_kernel(const float* __restrict__ qkv,
 // ------------------------------------------------------------- cmn_rows ---
 // Block = (64 channels, utterance); 4 row groups of 64 lanes: coalesced
 // 256-B row segments, partial sums combined through LDS.
-__global__ __launch_bounds__(256) void cmn_rows_kernel(float* __restrict__ x, int T, int D) {
+__global__ __launch_bounds__(256) void cmn_rows_kernel(float* __restrict__ x, int T_, int D,
+                                                       const int* __restrict__ seg) {
   __shared__ float part[4][64];
   const int b = blockIdx.y, c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
-  float* p = x + (size_t)b * T * D + c;
+  const int T = seg ? seg[b + 1] - seg[b] : T_;
+  float* p = x + (seg ? (size_t)seg[b] : (size_t)b * T_) * D + c;
   float s = 0.f;
   if (c < D)
     for (int t = g; t < T; t += 4) s += p[(size_t)t * D];
@@ -311,21 +338,30 @@ __global__ __launch_bounds__(256) void cmn_rows_kernel(float* __restrict__ x, in
 }  // namespace
 
 void launch_hubert_conv0(const float* wav, int B, int N, int ldw, int T0, const float* w, const float* gamma,
-                         const float* beta, double* stats, float* out, hipStream_t s) {
-  WSP_CHECK(B > 0 && T0 == (N - kK0) / kS0 + 1 && T0 > 0, "hubert conv0: bad frame count");
-  WSP_CHECK(ldw >= N, "hubert conv0: ldw < N");
+                         const float* beta, double* stats, float* out, hipStream_t s, const int* wseg,
+                         const int* oseg) {
+  WSP_CHECK((wseg == nullptr) == (oseg == nullptr), "hubert conv0: sample and row segments go together");
+  if (!wseg) {
+    WSP_CHECK(B > 0 && T0 == (N - kK0) / kS0 + 1 && T0 > 0, "hubert conv0: bad frame count");
+    WSP_CHECK(ldw >= N, "hubert conv0: ldw < N");
+  }
+  WSP_CHECK(B > 0 && T0 > 0, "hubert conv0: empty batch");  // segmented: T0 = longest utterance's frames
   WSP_HIP(hipMemsetAsync(stats, 0, sizeof(double) * 2 * B * kC0, s));
   const dim3 grid((T0 + kTC - 1) / kTC, B);
-  hipLaunchKernelGGL(conv0_kernel<0>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B);
-  hipLaunchKernelGGL(conv0_kernel<1>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B);
-  hipLaunchKernelGGL(conv0_kernel<2>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B);
+  hipLaunchKernelGGL(conv0_kernel<0>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B, wseg,
+                     oseg);
+  hipLaunchKernelGGL(conv0_kernel<1>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B, wseg,
+                     oseg);
+  hipLaunchKernelGGL(conv0_kernel<2>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B, wseg,
+                     oseg);
   WSP_HIP(hipGetLastError());
 }
 
 void launch_layernorm(const LayerNormArgs& p, hipStream_t s) {
   WSP_CHECK(p.M > 0 && (p.D == 512 || p.D == 768), "layernorm: D must be 512 or 768");
   WSP_CHECK(!p.add || (p.gin > 0 && p.gout >= p.gin), "layernorm: bad add remap");
-  WSP_CHECK(!p.feat || (p.T > 0 && p.Tout > 0 && p.M % p.T == 0), "layernorm: bad featurizer shape");
+  WSP_CHECK(!p.feat || p.seg || (p.T > 0 && p.Tout > 0 && p.M % p.T == 0), "layernorm: bad featurizer shape");
+  WSP_CHECK(!p.seg || (p.fseg && p.nseg > 0), "layernorm: segmented featurizer needs output offsets");
   const dim3 grid((p.M + 3) / 4);
   if (p.D == 512)
     hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, s, p);
@@ -334,17 +370,19 @@ void launch_layernorm(const LayerNormArgs& p, hipStream_t s) {
   WSP_HIP(hipGetLastError());
 }
 
-void launch_mha(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s) {
+void launch_mha(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s,
+                const int* seg) {
   WSP_CHECK(dh == kDH, "mha: head dim must be 64");
   WSP_CHECK(B > 0 && T > 0 && H > 0 && ldq >= 3 * H * dh && ldq % 4 == 0 && ldo % 4 == 0, "mha: bad shape");
-  const dim3 grid((T + kQW * kWaves - 1) / (kQW * kWaves), H, B);
-  hipLaunchKernelGGL(mha_kernel, grid, dim3(256), 0, s, qkv, ldq, out, ldo, T, H * dh, 1.f / sqrtf((float)dh));
+  const dim3 grid((T + kQW * kWaves - 1) / (kQW * kWaves), H, B);  // segmented: T = longest utterance
+  hipLaunchKernelGGL(mha_kernel, grid, dim3(256), 0, s, qkv, ldq, out, ldo, T, H * dh, 1.f / sqrtf((float)dh),
+                     seg);
   WSP_HIP(hipGetLastError());
 }
 
-void launch_cmn_rows(float* x, int B, int T, int D, hipStream_t s) {
-  WSP_CHECK(B > 0 && T > 0 && D > 0, "cmn: bad shape");
-  hipLaunchKernelGGL(cmn_rows_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, x, T, D);
+void launch_cmn_rows(float* x, int B, int T, int D, hipStream_t s, const int* seg) {
+  WSP_CHECK(B > 0 && (T > 0 || seg) && D > 0, "cmn: bad shape");
+  hipLaunchKernelGGL(cmn_rows_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, x, T, D, seg);
   WSP_HIP(hipGetLastError());
 }
 

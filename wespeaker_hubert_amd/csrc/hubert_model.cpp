@@ -146,34 +146,80 @@ int Model::Impl::hubert_cnn_frames(int N, int upto) const {
   return t;
 }
 
-// Utterances per feature-extractor chunk: the conv0 output (33 MB per 5 s
-// utterance) must stay below 2 GiB (32-bit buffer offsets).
-int Model::Impl::hubert_chunk(int B, int N) const {
-  const size_t per = (size_t)hubert_cnn_frames(N, 0) * kConvDim * sizeof(float);
-  int bc = (int)std::max<size_t>(1, ((size_t)1 << 31) / 8 * 7 / per);
-  bc = std::min(bc, B);
-  const int chunks = (B + bc - 1) / bc;
-  return (B + chunks - 1) / chunks;
+// Host-side plan of one (uniform or ragged) batch: frames per conv level,
+// feature-extractor chunks whose conv0 output stays below 2 GiB (32-bit buffer
+// offsets; 33 MB per 5 s utterance), and the int32 offset tables the kernels
+// read (uploaded into the workspace).
+HubertPlan Model::Impl::hubert_plan(int B, const int* lens) const {
+  HubertPlan pl;
+  pl.B = B;
+  std::vector<int> T[7], Tout(B);
+  for (int k = 0; k < 7; ++k) T[k].resize(B);
+  for (int b = 0; b < B; ++b) {
+    WSP_CHECK(lens[b] >= 400, "HuBERT needs at least 400 samples per utterance");
+    int t = lens[b];
+    for (int k = 0; k < 7; ++k) T[k][b] = t = (t - kConvK[k]) / kConvS[k] + 1;
+    Tout[b] = (lens[b] + kDownsample - 1) / kDownsample;
+  }
+  const size_t cap = ((size_t)1 << 31) / 8 * 7 / (kConvDim * sizeof(float));  // conv0 rows per chunk
+  for (int b0 = 0; b0 < B;) {
+    size_t rows = 0;
+    int b1 = b0;
+    while (b1 < B && (b1 == b0 || rows + T[0][b1] <= cap)) rows += T[0][b1++];
+    pl.chunks.push_back({b0, b1});
+    b0 = b1;
+  }
+  // offsets: global [seg6 | fseg], then per chunk [wseg | seg0 .. seg6] relative to the chunk
+  auto prefix = [&](const std::vector<int>& v, int lo, int hi) {
+    long long acc = 0;
+    pl.offs.push_back(0);
+    for (int b = lo; b < hi; ++b) {
+      acc += v[b];
+      WSP_CHECK(acc < (1LL << 31), "HuBERT batch too large");
+      pl.offs.push_back((int)acc);
+    }
+    return (size_t)acc;
+  };
+  pl.M = prefix(T[6], 0, B);
+  pl.Mout = prefix(Tout, 0, B);
+  std::vector<int> lv(lens, lens + B);
+  for (auto& c : pl.chunks) {
+    c.off = pl.offs.size();
+    c.samples = prefix(lv, c.b0, c.b1);
+    for (int k = 0; k < 7; ++k) c.rows[k] = prefix(T[k], c.b0, c.b1);
+    c.row6 = 0;
+    for (int b = 0; b < c.b0; ++b) c.row6 += T[6][b];
+    c.sample0 = 0;
+    for (int b = 0; b < c.b0; ++b) c.sample0 += lens[b];
+    c.maxT0 = *std::max_element(T[0].begin() + c.b0, T[0].begin() + c.b1);
+    pl.maxA = std::max(pl.maxA, c.rows[0]);
+    pl.maxB = std::max(pl.maxB, c.rows[1]);
+    pl.maxChunk = std::max(pl.maxChunk, c.b1 - c.b0);
+  }
+  pl.maxT6 = *std::max_element(T[6].begin(), T[6].end());
+  WSP_CHECK(pl.M * kFfn * sizeof(float) < ((size_t)1 << 31) - 64,
+            "HuBERT batch too large for one call (frames * 3072 floats must stay below 2 GiB)");
+  return pl;
 }
 
-size_t Model::Impl::hubert_ws_floats(int B, int N, size_t* offs) const {
-  const int bc = hubert_chunk(B, N);
-  const size_t T0 = hubert_cnn_frames(N, 0), T1 = hubert_cnn_frames(N, 1), T = hubert_cnn_frames(N, 6);
-  const size_t M = (size_t)B * T;
-  const size_t sizes[] = {bc * T0 * kConvDim, bc * T1 * kConvDim, (size_t)4 * bc * kConvDim,  // cnnA, cnnB, stats
-                          M * kHidden,        M * kHidden,        M * 3 * kHidden,           // x, x1, qkv
-                          M * kHidden,        M * kFfn};                                     // ao, ffn / pos
+size_t Model::Impl::hubert_ws_floats(const HubertPlan& pl, size_t* offs) const {
+  const size_t M = pl.M;
+  const size_t sizes[] = {pl.maxA * kConvDim, pl.maxB * kConvDim, (size_t)4 * pl.maxChunk * kConvDim,  // cnnA, cnnB, stats
+                          M * kHidden,        M * kHidden,        M * 3 * kHidden,                     // x, x1, qkv
+                          M * kHidden,        M * kFfn,                                                // ao, ffn / pos
+                          pl.offs.size()};                                                             // int32 offsets
   size_t o = 0;
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < 9; ++i) {
     if (offs) offs[i] = o;
     o += (sizes[i] + 63) / 64 * 64;
   }
   return o;
 }
 
-void Model::Impl::forward_hubert(const float* wav, int B, int N, float* feats, int cmn, float* ws, hipStream_t s) {
-  size_t off[8];
-  hubert_ws_floats(B, N, off);
+void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* feats, int cmn, float* ws,
+                                 hipStream_t s) {
+  size_t off[9];
+  hubert_ws_floats(pl, off);
   float* cnnA = ws + off[0];
   float* cnnB = ws + off[1];
   double* stats = reinterpret_cast<double*>(ws + off[2]);
@@ -183,25 +229,32 @@ void Model::Impl::forward_hubert(const float* wav, int B, int N, float* feats, i
   float* ao = ws + off[6];
   float* ffn = ws + off[7];
   float* pc = ffn;  // the pos_conv output is consumed before fc1 writes
-  const int T0 = hubert_cnn_frames(N, 0), T = hubert_cnn_frames(N, 6);
-  const int Tout = (N + kDownsample - 1) / kDownsample;
-  const int M = B * T;
-  const int bc = hubert_chunk(B, N);
+  int* dseg = reinterpret_cast<int*>(ws + off[8]);
+  // pageable source: the copy is staged before hipMemcpyAsync returns, so pl.offs may go away
+  WSP_HIP(hipMemcpyAsync(dseg, pl.offs.data(), pl.offs.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  const int B = pl.B;
+  const int M = (int)pl.M;
+  const int* seg6 = dseg;           // [B+1] hidden-state rows per utterance
+  const int* fseg = dseg + B + 1;   // [B+1] output feature rows per utterance
 
-  auto conv = [&](const char* tag, const ConvW& cw, const float* a, int lda, float* out, int ldo, int rows, int Tt,
-                  int Ti, int stride, int pad, int act, const float* res, bool bias, int gcols = 0, int gcin = 0) {
+  auto conv = [&](const char* tag, const ConvW& cw, const float* a, int lda, float* out, int ldo, int rows, int Ti,
+                  int stride, int pad, int act, const float* res, bool bias, const int* oseg, const int* iseg, int nseg,
+                  int gcols = 0, int gcin = 0) {
     ConvGemmArgs g{};
     g.a[0] = g.a[1] = g.a[2] = a;
     g.lda[0] = g.lda[1] = g.lda[2] = lda;
     g.cseg[0] = 0;
     g.cseg[1] = g.cseg[2] = g.cseg[3] = cw.cin;
-    fill(g, cw, rows, Tt, 1, pad, out, ldo, act, nullptr, bias);
+    fill(g, cw, rows, 1, 1, pad, out, ldo, act, nullptr, bias);
     g.stride = stride;
-    g.Ti = Ti;
+    g.Ti = oseg ? Ti : 1;  // row-local (taps 1) GEMMs: uniform T = Ti = 1 so input row == output row
     g.res = res;
     g.ldres = res ? ldo : 0;
     g.gcols = gcols;
     g.gcin = gcin;
+    g.seg = oseg;  // taps==1 projections pass null: row-local, no utterance structure needed
+    g.iseg = iseg;
+    g.nseg = nseg;
     run(tag, 2.0 * rows * (gcols ? (double)cw.N * kPosGin / kPosGout : cw.N) * cw.K, s, [&] { launch(g, cw, s); });
   };
   auto ln = [&](const char* tag, const float* in, const float* add, float* out, int rows, int D, const float* gm,
@@ -225,47 +278,48 @@ void Model::Impl::forward_hubert(const float* wav, int B, int N, float* feats, i
       a.feat = feats;
       a.feat_w = h_fw[layer];
       a.feat_init = (h_layer_sel >= 0 || layer == 0) ? 1 : 0;
-      a.T = T;
-      a.Tout = Tout;
+      a.seg = seg6;
+      a.fseg = fseg;
+      a.nseg = B;
     }
     run(tag, 0, s, [&] { launch_layernorm(a, s); });
   };
 
-  // ---- feature extractor, utterance chunks of bc
-  for (int b0 = 0; b0 < B; b0 += bc) {
-    const int nb = std::min(bc, B - b0);
-    run("h_conv0", 2.0 * nb * T0 * kConvDim * 10, s, [&] {
-      launch_hubert_conv0(wav + (size_t)b0 * N, nb, N, N, T0, h_conv0_w, h_gn_g, h_gn_b, stats, cnnA, s);
+  // ---- feature extractor, utterance chunks
+  for (const HubertChunk& c : pl.chunks) {
+    const int nb = c.b1 - c.b0;
+    const int* cs = dseg + c.off;  // [wseg | seg0 .. seg6], each nb+1, relative to the chunk
+    auto lvl = [&](int k) { return cs + (size_t)(k + 1) * (nb + 1); };
+    run("h_conv0", 2.0 * c.rows[0] * kConvDim * 10, s, [&] {
+      launch_hubert_conv0(wav + c.sample0, nb, 0, 0, c.maxT0, h_conv0_w, h_gn_g, h_gn_b, stats, cnnA, s, cs, lvl(0));
     });
     float* src = cnnA;
     float* dst = cnnB;
-    int Ti = T0;
     for (int i = 1; i < 7; ++i) {
-      const int To = (Ti - kConvK[i]) / kConvS[i] + 1;
-      conv("h_cnn", h_conv[i], src, kConvDim, dst, kConvDim, nb * To, To, Ti, kConvS[i], 0, kActGelu, nullptr, false);
+      conv("h_cnn", h_conv[i], src, kConvDim, dst, kConvDim, (int)c.rows[i], (int)c.rows[i - 1], kConvS[i], 0,
+           kActGelu, nullptr, false, lvl(i), lvl(i - 1), nb);
       std::swap(src, dst);
-      Ti = To;
     }
-    ln("h_ln", src, nullptr, src, nb * T, kConvDim, h_ln0_g, h_ln0_b, -1);
-    conv("h_proj", h_proj, src, kConvDim, x + (size_t)b0 * T * kHidden, kHidden, nb * T, T, T, 1, 0, kActNone, nullptr,
-         true);
+    ln("h_ln", src, nullptr, src, (int)c.rows[6], kConvDim, h_ln0_g, h_ln0_b, -1);
+    conv("h_proj", h_proj, src, kConvDim, x + c.row6 * kHidden, kHidden, (int)c.rows[6], (int)c.rows[6], 1, 0,
+         kActNone, nullptr, true, nullptr, nullptr, 0);
   }
   // ---- encoder: x + GELU(pos_conv(x)) -> LN  (SamePad: pad 64, last output dropped)
-  conv("h_pos_conv", h_pos, x, kHidden, pc, kPosGroups * kPosGout, M, T, T, 1, kPosK / 2, kActGelu, nullptr, true,
-       kPosGout, kPosGin);
+  conv("h_pos_conv", h_pos, x, kHidden, pc, kPosGroups * kPosGout, M, M, 1, kPosK / 2, kActGelu, nullptr, true, seg6,
+       nullptr, B, kPosGout, kPosGin);
   ln("h_ln", x, pc, x, M, kHidden, h_enc_g, h_enc_b, 0);
   for (int l = 0; l < kLayers; ++l) {
     const HLayer& L = h_layers[l];
-    conv("h_qkv", L.qkv, x, kHidden, qkv, 3 * kHidden, M, T, T, 1, 0, kActNone, nullptr, true);
-    run("h_attn", 4.0 * B * kHeads * (double)T * T * (kHidden / kHeads), s,
-        [&] { launch_mha(qkv, 3 * kHidden, ao, kHidden, B, T, kHeads, kHidden / kHeads, s); });
-    conv("h_out_proj", L.out, ao, kHidden, x1, kHidden, M, T, T, 1, 0, kActNone, x, true);
+    conv("h_qkv", L.qkv, x, kHidden, qkv, 3 * kHidden, M, M, 1, 0, kActNone, nullptr, true, nullptr, nullptr, 0);
+    run("h_attn", 4.0 * B * kHeads * (double)pl.maxT6 * pl.maxT6 * (kHidden / kHeads), s,
+        [&] { launch_mha(qkv, 3 * kHidden, ao, kHidden, B, pl.maxT6, kHeads, kHidden / kHeads, s, seg6); });
+    conv("h_out_proj", L.out, ao, kHidden, x1, kHidden, M, M, 1, 0, kActNone, x, true, nullptr, nullptr, 0);
     ln("h_ln", x1, nullptr, x, M, kHidden, L.ln1_g, L.ln1_b, -1);
-    conv("h_fc1", L.fc1, x, kHidden, ffn, kFfn, M, T, T, 1, 0, kActGelu, nullptr, true);
-    conv("h_fc2", L.fc2, ffn, kFfn, x1, kHidden, M, T, T, 1, 0, kActNone, x, true);
+    conv("h_fc1", L.fc1, x, kHidden, ffn, kFfn, M, M, 1, 0, kActGelu, nullptr, true, nullptr, nullptr, 0);
+    conv("h_fc2", L.fc2, ffn, kFfn, x1, kHidden, M, M, 1, 0, kActNone, x, true, nullptr, nullptr, 0);
     ln("h_ln", x1, nullptr, x, M, kHidden, L.ln2_g, L.ln2_b, l + 1);
   }
-  if (cmn) run("h_cmn", 0, s, [&] { launch_cmn_rows(feats, B, Tout, kHidden, s); });
+  if (cmn) run("h_cmn", 0, s, [&] { launch_cmn_rows(feats, B, 0, kHidden, s, fseg); });
 }
 
 // ------------------------------------------------------------ Model API ---
@@ -280,21 +334,34 @@ int Model::out_frames(int N) const {
 size_t Model::frontend_workspace_bytes(int B, int N) const {
   WSP_CHECK(impl->hubert, "frontend_workspace_bytes: not a front-end handle");
   WSP_CHECK(B > 0 && N >= 400, "HuBERT needs B >= 1 and N >= 400 samples");
-  return impl->hubert_ws_floats(B, N, nullptr) * sizeof(float) + 256;
+  const std::vector<int> lens(B, N);
+  return frontend_workspace_bytes_segments(B, lens.data());
+}
+
+size_t Model::frontend_workspace_bytes_segments(int B, const int* lens) const {
+  WSP_CHECK(impl->hubert, "frontend_workspace_bytes: not a front-end handle");
+  WSP_CHECK(B > 0 && lens, "HuBERT needs B >= 1 utterances");
+  return impl->hubert_ws_floats(impl->hubert_plan(B, lens), nullptr) * sizeof(float) + 256;
 }
 
 void Model::forward_frontend(const float* wav, int B, int N, float* feats, int cmn, void* ws, size_t ws_bytes,
                              hipStream_t s) {
+  WSP_CHECK(B > 0 && N >= 400, "HuBERT needs B >= 1 and N >= 400 samples");
+  const std::vector<int> lens(B, N);
+  forward_frontend_segments(wav, B, lens.data(), feats, nullptr, cmn, ws, ws_bytes, s);
+}
+
+void Model::forward_frontend_segments(const float* wav, int B, const int* lens, float* feats, int* frame_offsets,
+                                      int cmn, void* ws, size_t ws_bytes, hipStream_t s) {
   Impl& m = *impl;
   WSP_CHECK(m.hubert, "forward_frontend: not a front-end handle");
   WSP_CHECK(m.finalized, "forward before finalize");
-  WSP_CHECK(B > 0 && N >= 400, "HuBERT needs B >= 1 and N >= 400 samples");
-  const size_t M = (size_t)B * m.hubert_cnn_frames(N, 6);
-  WSP_CHECK(M * kFfn * sizeof(float) < ((size_t)1 << 31) - 64,
-            "HuBERT batch too large for one call (B * frames * 3072 floats must stay below 2 GiB)");
-  WSP_CHECK(ws_bytes >= frontend_workspace_bytes(B, N), "workspace too small");
+  WSP_CHECK(B > 0 && lens, "HuBERT needs B >= 1 utterances");
+  const HubertPlan pl = m.hubert_plan(B, lens);
+  WSP_CHECK(ws_bytes >= m.hubert_ws_floats(pl, nullptr) * sizeof(float) + 256, "workspace too small");
+  if (frame_offsets) std::copy(pl.offs.begin() + B + 1, pl.offs.begin() + 2 * (B + 1), frame_offsets);
   float* wsf = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
-  m.forward_hubert(wav, B, N, feats, cmn, wsf, s);
+  m.forward_hubert(wav, pl, feats, cmn, wsf, s);
 }
 
 }  // namespace wsp

@@ -49,10 +49,12 @@ struct ConvGemmArgs {
   // (a block never straddles a group) and group g reads input channels
   // [g*gcin, g*gcin + cin).  gcols 0 = ungrouped.
   int gcols, gcin;
-  // Segmented (ragged) batch, 1-D stride-1 convs: utterance b owns rows
-  // [seg[b], seg[b+1]) (device int32 [nseg+1]); taps outside it read zero.
-  // null = uniform T.
+  // Segmented (ragged) batch, 1-D convs: utterance b owns output rows
+  // [seg[b], seg[b+1]) and input rows [iseg[b], iseg[b+1]) (device int32
+  // [nseg+1]; iseg null = seg, stride 1); taps outside it read zero.
+  // seg null = uniform T.
   const int* seg;
+  const int* iseg;
   int nseg;
 };
 
@@ -132,8 +134,11 @@ void launch_fbank(const void* wav, int dtype, int B, int N, int ld, float scale,
 // HuBERT-base front end (hubert.hip).
 // conv0 (1 -> 512, k10 s5, no bias) + GroupNorm(512, 512) + GELU:
 // wav [B][ldw] (N samples) -> out [B][T0][512]; stats = [2][B][512] doubles scratch.
+// Segmented: wseg / oseg = device int32 [B+1] sample / output-row offsets, T0 = frames of
+// the longest utterance.
 void launch_hubert_conv0(const float* wav, int B, int N, int ldw, int T0, const float* w, const float* gamma,
-                         const float* beta, double* stats, float* out, hipStream_t s);
+                         const float* beta, double* stats, float* out, hipStream_t s, const int* wseg = nullptr,
+                         const int* oseg = nullptr);
 // out[row] = LayerNorm(x[row] (+ add[row][remap(c)])) with remap(c) = (c/gin)*gout + c%gin;
 // if feat: feat[b][t'] (=|+=) feat_w * out[row] for t' = t, and t' in [T, Tout) when t = T-1.
 struct LayerNormArgs {
@@ -150,12 +155,17 @@ struct LayerNormArgs {
   float* feat;
   float feat_w;
   int feat_init, T, Tout;
+  // segmented featurizer: hidden-state rows [seg[b], seg[b+1]) -> feature rows [fseg[b], fseg[b+1])
+  const int* seg;
+  const int* fseg;
+  int nseg;
 };
 void launch_layernorm(const LayerNormArgs& p, hipStream_t s);
 // softmax(Q K^T / sqrt(dh)) V per (utterance, head); qkv [B*T][ldq] = [q | k | v] (H*dh each).
-void launch_mha(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s);
+void launch_mha(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s,
+                const int* seg = nullptr);
 // x [B][T][D] -= mean over T  (apply_cmvn(norm_mean=True, norm_var=False))
-void launch_cmn_rows(float* x, int B, int T, int D, hipStream_t s);
+void launch_cmn_rows(float* x, int B, int T, int D, hipStream_t s, const int* seg = nullptr);
 
 // Scoring helpers.
 void launch_l2_normalize(const float* x, const float* sub, float* y, int R, int D, hipStream_t s);

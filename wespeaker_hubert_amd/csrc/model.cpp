@@ -191,7 +191,8 @@ void Model::profile_query(const std::string& tag, int* launches, double* total_m
     *total_ms += ms;
   }
   *launches = (int)e.used;
-  *flops = e.flops;
+  *flops = e.used ? e.flops / (double)e.used : 0.0;
+  e.flops = 0;
   e.used = 0;
 }
 

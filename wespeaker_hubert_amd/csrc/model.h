@@ -28,6 +28,11 @@ class Model {
   size_t frontend_workspace_bytes(int B, int N) const;
   void forward_frontend(const float* wav, int B, int N, float* feats, int cmn, void* ws, size_t ws_bytes,
                         hipStream_t s);
+  // ragged batch: utterance b = lens[b] samples (host array) of the concatenated wav;
+  // feats rows [frame_offsets[b], frame_offsets[b+1]) (host [B+1] out, may be null)
+  size_t frontend_workspace_bytes_segments(int B, const int* lens) const;
+  void forward_frontend_segments(const float* wav, int B, const int* lens, float* feats, int* frame_offsets, int cmn,
+                                 void* ws, size_t ws_bytes, hipStream_t s);
   // Segmented (ragged) batch: utterance b = feats rows [seg[b], seg[b+1]) (device int32
   // [B+1]), M = seg[B] rows in total.  ECAPA-TDNN only.
   size_t workspace_bytes_segments(int B, int M) const;

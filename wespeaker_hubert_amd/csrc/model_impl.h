@@ -79,6 +79,23 @@ inline float bf2f(uint16_t b) {
 
 using namespace detail;
 
+// HuBERT batch plan (hubert_model.cpp): utterance ranges of the feature
+// extractor, their row counts per conv level, and the int32 offset tables.
+struct HubertChunk {
+  int b0 = 0, b1 = 0;
+  size_t off = 0;       // index of this chunk's tables in HubertPlan::offs
+  size_t rows[7] = {};  // conv-level frame rows of the chunk
+  size_t samples = 0, sample0 = 0, row6 = 0;
+  int maxT0 = 0;
+};
+struct HubertPlan {
+  int B = 0;
+  size_t M = 0, Mout = 0, maxA = 0, maxB = 0;
+  int maxChunk = 0, maxT6 = 0;
+  std::vector<HubertChunk> chunks;
+  std::vector<int> offs;
+};
+
 struct Param {
   std::string name;
   std::vector<int64_t> shape;
@@ -155,9 +172,9 @@ struct Model::Impl {
   void build_hubert_params();
   void finalize_hubert();
   int hubert_cnn_frames(int N, int upto) const;
-  int hubert_chunk(int B, int N) const;
-  size_t hubert_ws_floats(int B, int N, size_t* offs) const;
-  void forward_hubert(const float* wav, int B, int N, float* feats, int cmn, float* ws, hipStream_t s);
+  HubertPlan hubert_plan(int B, const int* lens) const;
+  size_t hubert_ws_floats(const HubertPlan& pl, size_t* offs) const;
+  void forward_hubert(const float* wav, const HubertPlan& pl, float* feats, int cmn, float* ws, hipStream_t s);
 
   // segmented (ragged) forward in progress: device row offsets [cur_nseg + 1]
   const int* cur_seg = nullptr;
@@ -584,7 +601,7 @@ struct Model::Impl {
       e.ev.emplace_back(a, b);
     }
     auto& pr = e.ev[e.used++];
-    e.flops = flops;
+    e.flops += flops;  // summed; profile_query reports the mean per launch
     WSP_HIP(hipEventRecord(pr.first, s));
     f();
     WSP_HIP(hipEventRecord(pr.second, s));

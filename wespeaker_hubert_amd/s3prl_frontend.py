@@ -9,15 +9,18 @@ Weights arrive under the reference checkpoint's names
 the module-local form without the `frontend.` prefix is accepted too).
 
 Implemented: upstream name `hubert_base` (alias `hubert`), normalize=False,
-equal-length batches (what bin/extract.py:100-102 feeds), multilayer_feature /
+equal-length batches (what bin/extract.py:100-102 feeds), ragged batches of whole
+utterances (`extract_segments`: every utterance computed as if alone — GroupNorm,
+pos-conv padding, attention and featurizer all per utterance), multilayer_feature /
 layer selection.  s3prl itself is absent offline, so its glue (length match,
 Featurizer) is restated — see oracle/hubert_ref.py for the pinning status.
 """
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -108,6 +111,29 @@ class S3prlFrontend(_HipHandle):
         _lib.check(_lib.load().wsp_frontend_forward(self._handle, wavs.data_ptr(), B, W, out.data_ptr(), int(cmn),
                                                     ws.data_ptr(), ws.numel(), stream), "wsp_frontend_forward")
         return out
+
+    def extract_segments(self, wavs, cmn: bool = False) -> Tuple[torch.Tensor, List[int]]:
+        """Ragged batch of whole utterances (sequence of 1-D [-1, 1] waveforms, >= 400
+        samples each) -> (feats [sum_b T_b][768] on the device, frame offsets [B+1]);
+        rows of utterance b equal extract(wavs[b][None])[0]."""
+        dev = torch.device("cuda", self._device if self._device is not None else torch.cuda.current_device())
+        if self._handle is None:
+            self.to(dev)
+        lens = np.asarray([int(len(w)) for w in wavs], dtype=np.int32)
+        cat = torch.cat([torch.as_tensor(w).reshape(-1).to(torch.float32) for w in wavs]).to(dev)
+        nb = ctypes.c_size_t()
+        lib = _lib.load()
+        _lib.check(lib.wsp_frontend_workspace_bytes_segments(self._handle, len(lens), lens.ctypes.data,
+                                                             ctypes.byref(nb)), "wsp_frontend_workspace_bytes_segments")
+        total = int(sum((int(n) + 319) // 320 for n in lens))
+        feats = torch.empty(total, self.output_size(), dtype=torch.float32, device=dev)
+        offs = np.zeros(len(lens) + 1, dtype=np.int32)
+        ws = self._workspace_tensor(nb.value, dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(lib.wsp_frontend_forward_segments(self._handle, cat.data_ptr(), len(lens), lens.ctypes.data,
+                                                     feats.data_ptr(), offs.ctypes.data, int(cmn), ws.data_ptr(),
+                                                     ws.numel(), stream), "wsp_frontend_forward_segments")
+        return feats, offs.tolist()
 
     def forward(self, input: torch.Tensor, input_lengths: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """s3prl.py:80-93: (wavs (B, W), wavs_len (B,)) -> (feats (B, T, 768), feats_lens (B,))."""
