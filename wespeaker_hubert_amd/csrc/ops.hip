@@ -119,14 +119,87 @@ __global__ __launch_bounds__(256) void frame_stats_kernel(const float* __restric
     out[(long)b * ldo + std_off + c] = sqrtf(v + 1e-7f);
   }
 }
+
+// Vector form (C, ldx multiples of 4): a lane owns 4 channels (16-B loads), a
+// wave every 4th frame, 4 frames in flight per lane with independent partial
+// sums — the scalar kernel keeps one dependent 4-B load per lane in flight.
+__global__ __launch_bounds__(256) void frame_stats4_kernel(const float* __restrict__ x, int ldx, int T_,
+                                                           int C, float* __restrict__ out, int ldo,
+                                                           int with_std, int std_off,
+                                                           const int* __restrict__ seg) {
+  __shared__ f32x4 part[4][64];
+  __shared__ f32x4 s_mean[64];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = (blockIdx.y * 64 + lane) * 4;
+  const bool ok = c < C;
+  const int T = seg ? seg[b + 1] - seg[b] : T_;
+  const float* xb = x + (seg ? (long)seg[b] : (long)b * T_) * ldx + (ok ? c : 0);
+  auto row = [&](int t) { return *reinterpret_cast<const f32x4*>(xb + (long)t * ldx); };
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  f32x4 s0 = z, s1 = z, s2 = z, s3 = z;
+  int t = wave;
+  if (ok) {
+    for (; t + 12 < T; t += 16) {
+      s0 += row(t);
+      s1 += row(t + 4);
+      s2 += row(t + 8);
+      s3 += row(t + 12);
+    }
+    for (; t < T; t += 4) s0 += row(t);
+  }
+  part[wave][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  const float inv = 1.f / (float)T;
+  if (wave == 0) {
+    const f32x4 m = (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) * inv;
+    s_mean[lane] = m;
+    if (ok) *reinterpret_cast<f32x4*>(out + (long)b * ldo + c) = m;
+  }
+  __syncthreads();
+  if (!with_std) return;
+  const f32x4 m = s_mean[lane];
+  f32x4 q0 = z, q1 = z;
+  t = wave;
+  if (ok) {
+    for (; t + 4 < T; t += 8) {
+      const f32x4 d0 = row(t) - m, d1 = row(t + 4) - m;
+      q0 += d0 * d0;
+      q1 += d1 * d1;
+    }
+    for (; t < T; t += 4) {
+      const f32x4 d = row(t) - m;
+      q0 += d * d;
+    }
+  }
+  __syncthreads();
+  part[wave][lane] = q0 + q1;
+  __syncthreads();
+  if (wave == 0 && ok) {
+    const f32x4 v = (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) / (float)(T - 1);
+    f32x4 r;
+    for (int e = 0; e < 4; ++e) r[e] = sqrtf(v[e] + 1e-7f);
+    float* o = out + (long)b * ldo + std_off + c;
+    if (((ldo | std_off) & 3) == 0) *reinterpret_cast<f32x4*>(o) = r;
+    else for (int e = 0; e < 4; ++e) o[e] = r[e];
+  }
+}
 }  // namespace
 
 void launch_frame_stats(const float* x, int ldx, int B, int T, int C, float* out, int ldo,
                         int with_std, int std_off, hipStream_t s, const int* seg) {
   if (B == 0) return;
-  dim3 grid(B, ceil_div(C, 64));
-  hipLaunchKernelGGL(frame_stats_kernel, grid, dim3(256), 0, s, x, ldx, T, C, out, ldo, with_std,
-                     std_off, seg);
+  const bool vec = C % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  if (vec) {
+    dim3 grid(B, ceil_div(C, 256));
+    hipLaunchKernelGGL(frame_stats4_kernel, grid, dim3(256), 0, s, x, ldx, T, C, out, ldo, with_std, std_off,
+                       seg);
+  } else {
+    dim3 grid(B, ceil_div(C, 64));
+    hipLaunchKernelGGL(frame_stats_kernel, grid, dim3(256), 0, s, x, ldx, T, C, out, ldo, with_std,
+                       std_off, seg);
+  }
   WSP_HIP(hipGetLastError());
 }
 
@@ -215,13 +288,85 @@ __global__ __launch_bounds__(256) void astp_pool_kernel(const float* __restrict_
     out[(long)b * 2 * C + C + c] = sqrtf(fmaxf(var, 1e-7f));
   }
 }
+
+// Vector form (C % 4 == 0): 4 channels per lane (16-B loads of e and x), two
+// frames per step with their loads issued first, branch-free online softmax
+// (running max m, rescale exp(m - m') — two exps per element instead of a
+// per-lane branch).
+__global__ __launch_bounds__(256) void astp_pool4_kernel(const float* __restrict__ e,
+                                                         const float* __restrict__ x, int T_, int C,
+                                                         float* __restrict__ out, const int* __restrict__ seg) {
+  __shared__ f32x4 sm[4][4][64];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = (blockIdx.y * 64 + lane) * 4;
+  const bool ok = c < C;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  f32x4 mx = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, se = z, a1 = z, a2 = z;
+  const int T = seg ? seg[b + 1] - seg[b] : T_;
+  auto step = [&](const f32x4& ev, const f32x4& xv) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float m1 = fmaxf(mx[k], ev[k]);
+      const float sc = __expf(mx[k] - m1);  // 0 on the first frame (mx = -inf)
+      const float pe = __expf(ev[k] - m1);
+      se[k] = fmaf(se[k], sc, pe);
+      a1[k] = fmaf(a1[k], sc, pe * xv[k]);
+      a2[k] = fmaf(a2[k], sc, pe * xv[k] * xv[k]);
+      mx[k] = m1;
+    }
+  };
+  if (ok) {
+    const long base = (seg ? (long)seg[b] : (long)b * T_) * C + c;
+    auto ld = [&](const float* p, int t) { return *reinterpret_cast<const f32x4*>(p + base + (long)t * C); };
+    int t = wave;
+    for (; t + 4 < T; t += 8) {
+      const f32x4 e0 = ld(e, t), x0 = ld(x, t), e1 = ld(e, t + 4), x1 = ld(x, t + 4);
+      step(e0, x0);
+      step(e1, x1);
+    }
+    if (t < T) step(ld(e, t), ld(x, t));
+  }
+  sm[wave][0][lane] = mx;
+  sm[wave][1][lane] = se;
+  sm[wave][2][lane] = a1;
+  sm[wave][3][lane] = a2;
+  __syncthreads();
+  if (wave == 0 && ok) {
+    f32x4 mean, sd;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float M = sm[0][0][lane][k];
+      for (int w = 1; w < 4; ++w) M = fmaxf(M, sm[w][0][lane][k]);
+      float S = 0.f, A1 = 0.f, A2 = 0.f;
+      for (int w = 0; w < 4; ++w) {
+        const float m = sm[w][0][lane][k];
+        const float f = (m == -INFINITY) ? 0.f : __expf(m - M);
+        S += sm[w][1][lane][k] * f;
+        A1 += sm[w][2][lane][k] * f;
+        A2 += sm[w][3][lane][k] * f;
+      }
+      mean[k] = A1 / S;
+      sd[k] = sqrtf(fmaxf(A2 / S - mean[k] * mean[k], 1e-7f));
+    }
+    *reinterpret_cast<f32x4*>(out + (long)b * 2 * C + c) = mean;
+    *reinterpret_cast<f32x4*>(out + (long)b * 2 * C + C + c) = sd;
+  }
+}
 }  // namespace
 
 void launch_astp_pool(const float* e, const float* x, int B, int T, int C, float* out,
                       hipStream_t s, const int* seg) {
   if (B == 0) return;
-  dim3 grid(B, ceil_div(C, 64));
-  hipLaunchKernelGGL(astp_pool_kernel, grid, dim3(256), 0, s, e, x, T, C, out, seg);
+  const bool vec = C % 4 == 0 && ((reinterpret_cast<uintptr_t>(e) | reinterpret_cast<uintptr_t>(x) |
+                                   reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+  if (vec) {
+    dim3 grid(B, ceil_div(C, 256));
+    hipLaunchKernelGGL(astp_pool4_kernel, grid, dim3(256), 0, s, e, x, T, C, out, seg);
+  } else {
+    dim3 grid(B, ceil_div(C, 64));
+    hipLaunchKernelGGL(astp_pool_kernel, grid, dim3(256), 0, s, e, x, T, C, out, seg);
+  }
   WSP_HIP(hipGetLastError());
 }
 
