@@ -194,29 +194,73 @@ struct ALoader2D {
 
 // Shared GEMM epilogue for a wave's TM x TN tiles of 32x32 accumulators
 // (gfx950 32x32 C/D map: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)).
-// Branch-free: buffer loads / stores with out-of-range offsets for rows >= M
-// (loads return 0, stores are dropped), every residual load issued before the
-// first use — no per-element exec branches and serialised round trips.
-//   y = act(acc + bias[n] + row_bias[row/T][n] + res[row][n]) * scale[n] + shift[n]
+//   y = act(acc + bias[n] + row_bias[utt(row)][n] + res[row][n]) * scale[n] + shift[n]
+// Branch-free per element: the launch-uniform choices (activation, per-utterance
+// bias) select one of eight straight-line store loops up front — per-element
+// uniform branches made the epilogue ~18 % of a K=1024 block (in-kernel
+// s_memtime stamps) — and a row's byte offset is the tile's base plus a
+// compile-time row step times 4*ldo (no per-element multiply).  Rows >= M get
+// out-of-range buffer offsets: loads return 0, stores are dropped.
+template <int TM, int TN, int ACT, bool RB>
+__device__ __forceinline__ void gemm_epilogue_store(const ConvGemmArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0,
+                                                    int wm, int wn, int lane) {
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
+  const int ldo4 = p.ldo * 4;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + (wn * TN + j) * 32 + r32;
+    const float bv = p.bias ? p.bias[col] : 0.f;
+    const float sc = p.scale ? p.scale[col] : 1.f;
+    const float sh = p.scale ? p.shift[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row0 = m0 + (wm * TM + i) * 32 + 4 * h;
+      const int lim = p.M - row0;  // rows row0 + rr with rr < lim exist
+      const int base = row0 * ldo4 + col * 4;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2);
+        float y = acc[i][j][r] + bv;
+        if constexpr (RB) {
+          const int row = row0 + rr;
+          const int rowc = row < p.M ? row : p.M - 1;
+          const int ub = p.seg ? seg_of(p.seg, p.nseg, rowc) : rowc / p.T;
+          y += p.row_bias[(size_t)ub * p.N + col];
+        }
+        if constexpr (ACT == kActRelu) y = fmaxf(y, 0.f);
+        else if constexpr (ACT == kActTanh) y = tanhf(y);
+        else if constexpr (ACT == kActGelu) y = 0.5f * y * (1.f + erff(y * 0.70710678118654752f));
+        y = y * sc + sh;
+        const int off = rr < lim ? base + rr * ldo4 : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, off, 0, 0);
+      }
+    }
+  }
+}
+
 template <int TM, int TN>
 __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0,
                                               int wm, int wn, int lane) {
   const int r32 = lane & 31;
   const int h = lane >> 5;
-  const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
   if (p.res) {
     // one 32-row tile at a time: TN*16 residual loads in flight (register budget)
     const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res);
+    const int ldr4 = p.ldres * 4;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      const int row0 = m0 + (wm * TM + i) * 32 + 4 * h;
+      const int lim = p.M - row0;
       float rv[TN][16];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = n0 + (wn * TN + j) * 32 + r32;
+        const int base = row0 * ldr4 + (n0 + (wn * TN + j) * 32 + r32) * 4;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = m0 + (wm * TM + i) * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
-          const int off = row < p.M ? (row * p.ldres + col) * 4 : kOOB;
+          const int q = (r & 3) + 8 * (r >> 2);
+          const int off = q < lim ? base + q * ldr4 : kOOB;
           rv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, off, 0, 0));
         }
       }
@@ -226,30 +270,19 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
         for (int r = 0; r < 16; ++r) acc[i][j][r] += rv[j][r];
     }
   }
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + (wn * TN + j) * 32 + r32;
-    const float bv = p.bias ? p.bias[col] : 0.f;
-    const float sc = p.scale ? p.scale[col] : 1.f;
-    const float sh = p.scale ? p.shift[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + (wm * TM + i) * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
-        float y = acc[i][j][r] + bv;
-        if (p.row_bias) {
-          const int rowc = row < p.M ? row : p.M - 1;
-          const int ub = p.seg ? seg_of(p.seg, p.nseg, rowc) : rowc / p.T;
-          y += p.row_bias[(size_t)ub * p.N + col];
-        }
-        if (p.act == kActRelu) y = fmaxf(y, 0.f);
-        else if (p.act == kActTanh) y = tanhf(y);
-        else if (p.act == kActGelu) y = 0.5f * y * (1.f + erff(y * 0.70710678118654752f));
-        y = y * sc + sh;
-        const int off = row < p.M ? (row * p.ldo + col) * 4 : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, off, 0, 0);
-      }
+  if (p.row_bias) {
+    switch (p.act) {
+      case kActRelu: gemm_epilogue_store<TM, TN, kActRelu, true>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActTanh: gemm_epilogue_store<TM, TN, kActTanh, true>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActGelu: gemm_epilogue_store<TM, TN, kActGelu, true>(p, acc, m0, n0, wm, wn, lane); break;
+      default: gemm_epilogue_store<TM, TN, kActNone, true>(p, acc, m0, n0, wm, wn, lane); break;
+    }
+  } else {
+    switch (p.act) {
+      case kActRelu: gemm_epilogue_store<TM, TN, kActRelu, false>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActTanh: gemm_epilogue_store<TM, TN, kActTanh, false>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActGelu: gemm_epilogue_store<TM, TN, kActGelu, false>(p, acc, m0, n0, wm, wn, lane); break;
+      default: gemm_epilogue_store<TM, TN, kActNone, false>(p, acc, m0, n0, wm, wn, lane); break;
     }
   }
 }
