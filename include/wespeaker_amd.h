@@ -25,6 +25,9 @@
  *                        bin/extract.py:114-116); C++ plugin analogue
  *                        SpeakerModel::ExtractEmbedding
  *                        (runtime/core/speaker/speaker_model.h:25-32)
+ *   wsp_cmn              cli/speaker.py:106-110 (subsegment CMN), dataset_utils.py:19-26
+ *   wsp_resample*        cli/speaker.py:155-157, dataset/processor.py:242-260
+ *                        (torchaudio.transforms.Resample)
  *   wsp_l2_normalize,
  *   wsp_cosine_pairs     bin/score.py:38-72 trials_cosine_score;
  *                        Speaker.cosine_similarity cli/speaker.py:189-192
@@ -167,6 +170,35 @@ int wsp_frontend_workspace_bytes_segments(const wsp_model* m, int B, const int32
 int wsp_frontend_forward_segments(wsp_model* m, const float* wav, int B, const int32_t* num_samples, float* feats,
                                   int32_t* frame_offsets, int cmn, void* workspace, size_t workspace_bytes,
                                   void* stream);
+
+/* Per-row mean subtraction over frames, in place: x [B][T][D] f32, x[b][t][:] -=
+ * mean_t x[b][t][:].  Replaces the subsegment CMN of Speaker.extract_embedding_feats
+ * (wespeaker/cli/speaker.py:106-110, np.mean over axis 1) and apply_cmvn(norm_mean)
+ * (wespeaker/dataset/dataset_utils.py:19-26) on feature tensors already on the device. */
+int wsp_cmn(float* x, int B, int T, int D, void* stream);
+
+/* --------------------------------------------------------- resampling --- */
+/* Replaces torchaudio.transforms.Resample(orig_freq, new_freq) as the reference
+ * applies it before fbank (wespeaker/cli/speaker.py:155-157) and in the data
+ * pipeline (wespeaker/dataset/processor.py:242-260): band-limited sinc with a
+ * Hann window (torchaudio's default "sinc_interp_hann"; lowpass_filter_width 6,
+ * rolloff 0.99 reproduce Resample's defaults).  create() builds the kernel on
+ * the host; resample() maps
+ * x [B][num_samples] (row stride ld) to y [B][out_len] (row stride ldy),
+ * out_len = ceil(new * num_samples / orig) after reducing the rates by their gcd;
+ * orig == new copies x. */
+typedef struct wsp_resampler wsp_resampler;
+int wsp_resampler_create(int orig_freq, int new_freq, int lowpass_filter_width, float rolloff,
+                         wsp_resampler** out);
+int wsp_resampler_destroy(wsp_resampler* r);
+int wsp_resampler_out_len(const wsp_resampler* r, int num_samples, int* out_len);
+int wsp_resample(const wsp_resampler* r, const float* x, int B, int num_samples, int ld, float* y, int ldy,
+                 void* stream);
+/* Host copy of the plan: reduced rates, half-width, taps per phase and (kernel
+ * != NULL) the [reduced_new][taps] f32 kernel.  Creation is host-only; the
+ * device copy is made by the first wsp_resample on the then-current device. */
+int wsp_resampler_kernel(const wsp_resampler* r, int* reduced_orig, int* reduced_new, int* width, int* taps,
+                         float* kernel);
 
 /* ------------------------------------------------------------ scoring --- */
 /* y[r] = x[r] - sub (sub may be NULL), then L2-normalised; [R][D] f32. */

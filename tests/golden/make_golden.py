@@ -44,8 +44,9 @@ def _import_reference():
     pkg.__path__ = [os.path.join(REF, "wespeaker")]
     sys.modules["wespeaker"] = pkg
     # import-only stubs: score_norm imports fire + kaldiio at module level but
-    # get_mean_std never touches them.
-    for stub in ("fire", "kaldiio"):
+    # get_mean_std never touches them; diar/extract_emb imports
+    # kaldiio + onnxruntime at module level, its subsegment() uses numpy only.
+    for stub in ("fire", "kaldiio", "onnxruntime"):
         if stub not in sys.modules:
             sys.modules[stub] = types.ModuleType(stub)
     from wespeaker.models import ecapa_tdnn, pooling_layers, resnet  # noqa
@@ -135,6 +136,36 @@ def make_pooling(out):
     print("pooling", {k: v.shape for k, v in res.items() if hasattr(v, "shape")})
 
 
+# (segment id, frames, window_fs, period_fs): shorter than a window, exact
+# multiples, ragged tails, the reference's "+2 frames" id/fbank mismatch
+DIAR_CASES = [
+    ("spk1-utt1-00000000-00001000", 98, 150, 75),
+    ("spk1-utt1-00001000-00002500", 148, 150, 75),
+    ("spk2-utt7-00000120-00004730", 459, 150, 75),
+    ("spk2-utt7-00010000-00013330", 331, 150, 75),
+    ("spk3-utt2-00000000-00006000", 598, 150, 50),
+    ("spk3-utt2-00000000-00001510", 149, 150, 75),
+]
+
+
+def make_diar(out):
+    """diar/extract_emb.py:55-83 subsegment() on synthetic fbanks."""
+    import importlib
+    _import_reference()
+    extract_emb = importlib.import_module("wespeaker.diar.extract_emb")
+    rng = np.random.default_rng(77)
+    arrays = {}
+    for n, (seg_id, frames, win, per) in enumerate(DIAR_CASES):
+        fb = rng.standard_normal((frames, 8)).astype(np.float32)  # any feature dim
+        ids, wins = extract_emb.subsegment(fb, seg_id, win, per, 10)
+        arrays[f"fbank_{n}"] = fb
+        arrays[f"ids_{n}"] = np.array(ids)
+        arrays[f"wins_{n}"] = np.stack(wins).astype(np.float32)
+        arrays[f"case_{n}"] = np.array([seg_id, str(win), str(per)])
+    np.savez_compressed(os.path.join(out, "diar_subsegment.npz"), **arrays)
+    print("diar cases", len(DIAR_CASES))
+
+
 def make_scoring(out):
     _, _, _, score_norm, score_metrics = _import_reference()
     rng = np.random.default_rng(401)
@@ -162,10 +193,12 @@ def make_scoring(out):
 
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 1)
-    what = sys.argv[1:] or ["models", "pooling", "scoring"]
+    what = sys.argv[1:] or ["models", "pooling", "scoring", "diar"]
     if "pooling" in what:
         make_pooling(HERE)
     if "scoring" in what:
         make_scoring(HERE)
+    if "diar" in what:
+        make_diar(HERE)
     if "models" in what:
         make_models(HERE)

@@ -90,6 +90,41 @@ def test_load_model_extract_embedding_list(model_dir, wav_scp):
     assert abs(sim - (_cos(e0, e1) + 1) / 2) < 1e-4
 
 
+def test_extract_embedding_feats_diar_windows(model_dir, wav_scp):
+    """Speaker.extract_embedding_feats (speaker.py:106-121) on diar.subsegment
+    windows: subsegment CMN on the device (wsp_cmn), batches of 7, vs the oracle
+    model on numpy-CMN'd windows one at a time."""
+    import wespeaker_hubert_amd as wespeaker
+    from wespeaker_hubert_amd.diar import subsegment
+    d, sd = model_dir
+    _, _, pcms = wav_scp
+    spk = wespeaker.load_model(d)
+    ids, wins = [], []
+    for k in ("u04", "u06"):  # 3.0 s and 2.5 s segments -> 1.5 s windows every 0.75 s
+        fb = fbank_ref.fbank(pcms[k], cmn=False)
+        seg_id = f"{k}-00000000-{(fb.shape[0] + 2) * 10:08d}"
+        i, w = subsegment(fb, seg_id, 150, 75, 10)
+        ids += i
+        wins += w
+    assert len(wins) >= 5
+    embs = spk.extract_embedding_feats(wins, batch_size=7, subseg_cmn=True)
+    assert embs.shape == (len(wins), 192) and embs.dtype == np.float32
+    sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
+    for n, w in enumerate(wins):
+        x = w - np.mean(w, axis=0, keepdims=True)
+        with torch.no_grad():
+            _, ref = models_ref.forward(ARCH, torch.from_numpy(x[None].astype(np.float32)), sdt)
+        ref = ref[0].numpy()
+        # embeddings are O(10-40) here: fp32-level agreement relative to their scale
+        assert _cos(embs[n], ref) >= 0.99999
+        assert np.abs(embs[n] - ref).max() <= 2e-5 * max(1.0, float(np.abs(ref).max()))
+    raw = spk.extract_embedding_feats(wins[:3], batch_size=2, subseg_cmn=False)
+    with torch.no_grad():
+        _, ref = models_ref.forward(ARCH, torch.from_numpy(np.stack(wins[:3]).astype(np.float32)), sdt)
+    ref = ref.numpy()
+    assert np.abs(raw - ref).max() <= 2e-5 * max(1.0, float(np.abs(ref).max()))
+
+
 def test_cli_embedding_kaldi(model_dir, wav_scp, tmp_path):
     from wespeaker_hubert_amd.cli.speaker import main
     d, sd = model_dir

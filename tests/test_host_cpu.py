@@ -1,4 +1,6 @@
 """Host-side logic that needs no GPU: registry, state_dict intake, errors."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -75,3 +77,19 @@ def test_ragged_pack_groups_are_contiguous_and_bounded():
         assert hi - lo == 1 or sum(frames[lo:hi]) <= 600
     got = list(stream_groups(((str(i), np.zeros(n)) for i, n in enumerate(lens)), 600))
     assert [len(k) for k, _ in got] == [hi - lo for lo, hi in groups]
+
+
+# ---------------------------------------------------------------- diarization --
+def test_subsegment_matches_reference_fixture():
+    """diar.subsegment vs the reference's diar/extract_emb.py:55-83 on the cases in
+    tests/golden/diar_subsegment.npz (made by make_golden.py diar)."""
+    from wespeaker_hubert_amd.diar import subsegment
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "diar_subsegment.npz"))
+    n = 0
+    while f"case_{n}" in z:
+        seg_id, win, per = z[f"case_{n}"]
+        ids, wins = subsegment(z[f"fbank_{n}"], str(seg_id), int(win), int(per), 10)
+        assert ids == [str(x) for x in z[f"ids_{n}"]]
+        np.testing.assert_array_equal(np.stack(wins), z[f"wins_{n}"])
+        n += 1
+    assert n == 6

@@ -51,6 +51,12 @@ SIGNATURES = {
     "wsp_model_profile": (c_int, [c_void_p, c_int]),
     "wsp_model_profile_query": (c_int, [c_void_p, c_char_p, POINTER(c_int), POINTER(c_double),
                                         POINTER(c_double)]),
+    "wsp_cmn": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "wsp_resampler_create": (c_int, [c_int, c_int, c_int, c_float, c_void_p]),
+    "wsp_resampler_destroy": (c_int, [c_void_p]),
+    "wsp_resampler_out_len": (c_int, [c_void_p, c_int, c_void_p]),
+    "wsp_resample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "wsp_resampler_kernel": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "wsp_l2_normalize": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "wsp_cosine_pairs": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "wsp_asnorm_stats": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,

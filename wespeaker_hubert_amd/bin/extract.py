@@ -44,6 +44,7 @@ from ..batching import DEFAULT_MAX_FRAMES, embed_utterances, stream_groups
 from ..dist import shard_lines
 from ..frontend import compute_fbank
 from ..kaldi_io import WriteHelper, validate_path
+from ..resample import resample
 from ..s3prl_frontend import S3prlFrontend
 from ..speaker_model import get_speaker_model
 from . import _fire
@@ -190,9 +191,11 @@ def extract(config="conf/config.yaml", **kwargs):
             writer(k, e)
 
     def checked(items):
+        # processor.py:242-260 `resample`: torchaudio.transforms.Resample(sr, resample_rate)
+        # before chunking / fbank, here on the device (resample.Resample)
         for key, x, sr in items:
             if sr != sr_target:
-                raise NotImplementedError(f"{key}: sample rate {sr} != {sr_target} (resampling not implemented)")
+                x = resample(torch.from_numpy(np.asarray(x, np.float32)).to(device), sr, sr_target).cpu().numpy()
             yield key, x
 
     n = 0

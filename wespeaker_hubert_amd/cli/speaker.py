@@ -8,7 +8,8 @@ Differences, all deliberate and documented in DESIGN.md:
   * `load_model(name)` never downloads (no network): the name must be a model
     directory (the reference's Hub path, cli/hub.py, is out of scope);
   * VAD (silero) and diarization are out of scope: `set_vad(True)` and
-    `diarize*` raise NotImplementedError; resampling other than 16 kHz raises.
+    `diarize*` raise NotImplementedError; the diarization embedding batcher
+    `extract_embedding_feats` (+ diar.subsegment) is implemented.
 """
 from __future__ import annotations
 
@@ -23,8 +24,10 @@ import yaml
 
 from ..audio import load_wav
 from ..batching import embed_utterances
+from ..frontend import apply_cmn as _apply_cmn
 from ..frontend import compute_fbank as _gpu_fbank
 from ..kaldi_io import WriteHelper
+from ..resample import resample as _resample
 from ..speaker_model import get_speaker_model
 
 
@@ -78,20 +81,40 @@ class Speaker:
         """speaker.py:89-104 on the GPU; `wavform` (1, N) int16-valued."""
         if (sample_rate, num_mel_bins, frame_length, frame_shift) != (16000, 80, 25, 10):
             raise NotImplementedError("fbank implemented for 16 kHz, 80 bins, 25/10 ms")
-        x = torch.as_tensor(np.asarray(wavform), dtype=torch.float32).to(self.device)
+        if isinstance(wavform, torch.Tensor):
+            x = wavform.to(device=self.device, dtype=torch.float32)
+        else:
+            x = torch.as_tensor(np.asarray(wavform), dtype=torch.float32).to(self.device)
         if x.dim() == 2:
             x = x[:1]
         return _gpu_fbank(x, scale=1.0, cmn=cmn, window_type=self.window_type)[0]
 
     # -------------------------------------------------------- embeddings --
+    def extract_embedding_feats(self, fbanks, batch_size: int, subseg_cmn: bool) -> np.ndarray:
+        """speaker.py:106-121: embeddings of equal-length fbank windows (a list of
+        (T, F) arrays, e.g. diar.subsegment output) in batches of `batch_size`;
+        subseg_cmn subtracts each window's mean over frames first (wsp_cmn on the
+        device).  Returns an (N, D) float32 array."""
+        arr = np.ascontiguousarray(np.stack([np.asarray(f, dtype=np.float32) for f in fbanks]))
+        feats = torch.from_numpy(arr).to(self.device)
+        if subseg_cmn:
+            _apply_cmn(feats)
+        out = []
+        with torch.no_grad():
+            for i in range(0, feats.shape[0], batch_size):
+                emb = self.model(feats[i:i + batch_size])
+                emb = emb[-1] if isinstance(emb, tuple) else emb
+                out.append(emb.detach().cpu().numpy())
+        return np.vstack(out)
+
     def extract_embedding(self, audio_path: str):
         pcm, sample_rate = load_wav(audio_path, normalize=self.wavform_norm)
         return self.extract_embedding_from_pcm(torch.from_numpy(pcm), sample_rate)
 
     def extract_embedding_from_pcm(self, pcm: torch.Tensor, sample_rate: int):
         pcm = pcm.to(torch.float)
-        if sample_rate != self.resample_rate:
-            raise NotImplementedError("resampling is not implemented (16 kHz input expected)")
+        if sample_rate != self.resample_rate:  # speaker.py:155-157, on the device
+            pcm = _resample(pcm.to(self.device), sample_rate, self.resample_rate)
         feats = self.compute_fbank(pcm, sample_rate=self.resample_rate, cmn=True)
         feats = feats.unsqueeze(0)
         with torch.no_grad():
@@ -109,10 +132,12 @@ class Speaker:
                     continue
                 name, wav_path = line.strip().split()
                 pcm, sample_rate = load_wav(wav_path, normalize=self.wavform_norm)
+                pcm = pcm[0].astype(np.float32)
                 if sample_rate != self.resample_rate:
-                    raise NotImplementedError("resampling is not implemented (16 kHz input expected)")
+                    x = torch.from_numpy(pcm).to(self.device)
+                    pcm = _resample(x, sample_rate, self.resample_rate).cpu().numpy()
                 names.append(name)
-                pcms.append(pcm[0].astype(np.float32))
+                pcms.append(pcm)
         with torch.no_grad():
             embeddings = embed_utterances(self.model, pcms, self.device)
         return names, [np.asarray(e, dtype=np.float32) for e in embeddings]

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -238,6 +239,87 @@ int wsp_model_profile_query(wsp_model* m, const char* kernel_class, int* launche
   WSP_GUARD({
     WSP_CHECK(m && kernel_class && launches && total_ms && flops_per_launch, "null argument");
     m->m.profile_query(kernel_class, launches, total_ms, flops_per_launch);
+  });
+}
+
+struct wsp_resampler {
+  wsp::ResamplePlan plan;
+  // device copy of the kernel table, made on the first wsp_resample call
+  // (creation is host-only, like wsp_model_create)
+  mutable std::mutex mu;
+  mutable int device = -1;
+  mutable float* kern = nullptr;
+  mutable int* band = nullptr;
+};
+
+int wsp_resampler_create(int orig_freq, int new_freq, int lowpass_filter_width, float rolloff,
+                         wsp_resampler** out) {
+  WSP_GUARD({
+    WSP_CHECK(out != nullptr, "bad argument");
+    *out = nullptr;
+    auto r = std::make_unique<wsp_resampler>();
+    wsp::resample_plan(orig_freq, new_freq, lowpass_filter_width, rolloff, r->plan);
+    *out = r.release();
+  });
+}
+
+int wsp_resampler_destroy(wsp_resampler* r) {
+  WSP_GUARD({
+    if (r) {
+      if (r->kern) (void)hipFree(r->kern);
+      if (r->band) (void)hipFree(r->band);
+      delete r;
+    }
+  });
+}
+
+int wsp_resampler_out_len(const wsp_resampler* r, int num_samples, int* out_len) {
+  WSP_GUARD({
+    WSP_CHECK(r && out_len && num_samples >= 0, "bad argument");
+    const long long n = wsp::resample_out_len(r->plan, num_samples);
+    WSP_CHECK(n < (1LL << 31), "output too long");
+    *out_len = (int)n;
+  });
+}
+
+int wsp_resampler_kernel(const wsp_resampler* r, int* reduced_orig, int* reduced_new, int* width, int* taps,
+                         float* kernel) {
+  WSP_GUARD({
+    WSP_CHECK(r != nullptr, "bad argument");
+    if (reduced_orig) *reduced_orig = r->plan.orig;
+    if (reduced_new) *reduced_new = r->plan.nw;
+    if (width) *width = r->plan.width;
+    if (taps) *taps = r->plan.L;
+    if (kernel && !r->plan.identity) std::copy(r->plan.kern.begin(), r->plan.kern.end(), kernel);
+  });
+}
+
+int wsp_resample(const wsp_resampler* r, const float* x, int B, int num_samples, int ld, float* y, int ldy,
+                 void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(r && B >= 0 && num_samples >= 0 && (B == 0 || num_samples == 0 || (x && y)), "bad argument");
+    int dev = -1;
+    WSP_HIP(hipGetDevice(&dev));
+    if (!r->plan.identity) {
+      std::lock_guard<std::mutex> lk(r->mu);
+      if (r->device < 0) {
+        WSP_HIP(hipMalloc(&r->kern, r->plan.kern.size() * sizeof(float)));
+        WSP_HIP(hipMalloc(&r->band, r->plan.band.size() * sizeof(int)));
+        WSP_HIP(hipMemcpy(r->kern, r->plan.kern.data(), r->plan.kern.size() * sizeof(float),
+                          hipMemcpyHostToDevice));
+        WSP_HIP(hipMemcpy(r->band, r->plan.band.data(), r->plan.band.size() * sizeof(int), hipMemcpyHostToDevice));
+        r->device = dev;
+      }
+      WSP_CHECK(dev == r->device, "resampler is bound to another device");
+    }
+    wsp::launch_resample(r->plan, r->kern, r->band, x, B, num_samples, ld, y, ldy, S(stream));
+  });
+}
+
+int wsp_cmn(float* x, int B, int T, int D, void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(B >= 0 && T > 0 && D > 0 && (B == 0 || x), "bad argument");
+    if (B > 0) wsp::launch_cmn_rows(x, B, T, D, S(stream));
   });
 }
 

@@ -1,6 +1,8 @@
 // Launcher interfaces of the hand-written gfx950 kernels.
 #pragma once
 
+#include <vector>
+
 #include "common.h"
 
 namespace wsp {
@@ -176,5 +178,18 @@ void launch_asnorm_stats(const float* E, int Ne, const float* C, int Nc, int D, 
                          double* mu, double* sd, float* ws, hipStream_t s);
 void launch_row_mean_accum(const float* x, const int32_t* group, int R, int D, double* acc,
                            double* cnt, hipStream_t s);
+
+// ------------------------------------------------------------ resampling --
+// torchaudio.transforms.Resample (sinc_interp_hann) — resample.hip.
+struct ResamplePlan {
+  int orig = 1, nw = 1, width = 0, L = 1;  // reduced rates, half-width, taps per phase
+  bool identity = true;
+  std::vector<float> kern;  // [nw][L]
+  std::vector<int> band;    // [nw][2] nonzero tap range per phase
+};
+void resample_plan(int orig_freq, int new_freq, int lowpass_filter_width, double rolloff, ResamplePlan& p);
+long long resample_out_len(const ResamplePlan& p, long long n);
+void launch_resample(const ResamplePlan& p, const float* d_kern, const int* d_band, const float* x, int B, int N,
+                     long ldx, float* y, long ldy, hipStream_t s);
 
 }  // namespace wsp

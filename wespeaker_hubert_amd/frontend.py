@@ -73,3 +73,15 @@ def compute_fbank_segments(wavs, scale: float = 1.0, cmn: bool = True, device=No
                                               NUM_BINS, 16000, _lib.WSP_WINDOW_HAMMING, int(cmn), stream),
                "wsp_fbank_segments")
     return feats, fo, frames
+
+
+def apply_cmn(feats: torch.Tensor) -> torch.Tensor:
+    """In-place per-utterance mean subtraction over frames of a (B, T, D) float32
+    HIP tensor (wsp_cmn) — apply_cmvn(norm_mean=True, norm_var=False),
+    dataset_utils.py:19-26, and the subsegment CMN of extract_embedding_feats."""
+    if not feats.is_cuda or feats.dtype != torch.float32 or not feats.is_contiguous() or feats.dim() != 3:
+        raise ValueError("apply_cmn expects a contiguous (B, T, D) float32 HIP tensor")
+    B, T, D = feats.shape
+    stream = torch.cuda.current_stream(feats.device).cuda_stream
+    _lib.check(_lib.load().wsp_cmn(feats.data_ptr(), B, T, D, stream), "wsp_cmn")
+    return feats
