@@ -152,6 +152,7 @@ int conv_gemm_tile_for(int N) { return (N % 128 == 0) ? 0 : 1; }
 void launch_conv_gemm(const ConvGemmArgs& args, hipStream_t s) {
   const ConvGemmArgs p = normalized(args);
   check_conv_args(p, "conv_gemm");
+  WSP_CHECK(!p.colsum, "conv_gemm: column sums are a bf16x3-kernel epilogue");
   WSP_CHECK(!p.conv2d && p.N % 64 == 0, "conv_gemm (f32): 1-D convs with N % 64 == 0 only");
   WSP_CHECK(!p.gcols || p.gcols % 64 == 0, "conv_gemm (f32): grouped columns must be a multiple of 64");
   if (conv_gemm_tile_for(p.N) == 0 && !p.gcols)

@@ -236,13 +236,14 @@ void launch_d(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipSt
 }  // namespace
 
 bool conv_gemm_dma_supported(const ConvGemmArgs& p) {
-  return !p.conv2d && p.amode == kACat && p.N % 128 == 0 && (uniform_ktiles(p) || p.cseg[1] == p.cin) &&
+  return !p.colsum && !p.conv2d && p.amode == kACat && p.N % 128 == 0 && (uniform_ktiles(p) || p.cseg[1] == p.cin) &&
          p.stride <= 1 && (p.Ti == 0 || p.Ti == p.T) && !p.gcols && !p.seg;
 }
 
 void launch_conv_gemm_dma(const ConvGemmArgs& args, const void* whi, const void* wlo, hipStream_t s) {
   const ConvGemmArgs p = normalized(args);
   check_conv_args(p, "conv_gemm_dma");
+  WSP_CHECK(!p.colsum, "conv_gemm_dma: column sums are a bf16x3-kernel epilogue");
   WSP_CHECK(conv_gemm_dma_supported(p), "conv_gemm_dma: unsupported operand layout");
   const __bf16* h = static_cast<const __bf16*>(whi);
   const __bf16* l = static_cast<const __bf16*>(wlo);

@@ -197,7 +197,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
     __syncthreads();
   }
 
-  gemm_epilogue<TM, TN>(p, acc, m0, n0, wm, wn, lane);
+  gemm_epilogue<TM, TN, WM, WN>(p, acc, m0, n0, wm, wn, lane, smem);
 }
 
 template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D, bool SWZ>
@@ -234,10 +234,46 @@ void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo,
 
 }  // namespace
 
+int conv_gemm_x3_block_rows(const ConvGemmArgs& p, int variant) {
+  if (p.N % 64 != 0 || (p.gcols && p.gcols % 64 != 0)) return 128;
+  if (p.gcols || p.N % 128 != 0) return 128;
+  return (variant == 1 || variant == 4) ? 256 : 128;
+}
+
+namespace {
+__global__ __launch_bounds__(256) void colsum_mean_kernel(const double* __restrict__ part, int bm, int T, int N,
+                                                          float* __restrict__ out, int ldo) {
+  const int b = blockIdx.y;
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const long r0 = (long)b * T, r1 = r0 + T;  // utterance rows
+  double v = 0.0;
+  for (long mt = r0 / bm; mt * bm < r1; ++mt) {
+    const int slot = (mt * bm) / T == b ? 0 : 1;  // the block starts in utterance b, or in b-1
+    v += part[((size_t)mt * 2 + slot) * N + n];
+  }
+  out[(long)b * ldo + n] = (float)(v / (double)T);
+}
+}  // namespace
+
+void launch_colsum_mean(const double* part, int block_rows, int T, int B, int N, float* out, int ldo,
+                        hipStream_t s) {
+  WSP_CHECK(block_rows > 0 && T >= block_rows && B > 0 && N > 0, "colsum_mean: bad shape");
+  hipLaunchKernelGGL(colsum_mean_kernel, dim3((N + 255) / 256, B), dim3(256), 0, s, part, block_rows, T, N, out,
+                     ldo);
+  WSP_HIP(hipGetLastError());
+}
+
 void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* wlo, int variant,
                          hipStream_t s) {
   const ConvGemmArgs p = normalized(args);
   check_conv_args(p, "conv_gemm_x3");
+  if (p.colsum) {
+    const int bm = conv_gemm_x3_block_rows(p, variant);
+    WSP_CHECK(!p.seg && !p.row_bias && !p.conv2d && p.T >= bm && (variant == 1 || variant == 3 || variant == 4 ||
+                                                                  variant == 0),
+              "conv_gemm_x3: column sums need a uniform batch with T >= block rows and no row bias");
+  }
   WSP_CHECK(p.Kp % 64 == 0, "conv_gemm_x3: packed K must be a multiple of 64");
   const __bf16* h = static_cast<const __bf16*>(whi);
   const __bf16* l = static_cast<const __bf16*>(wlo);

@@ -201,9 +201,9 @@ struct ALoader2D {
 // s_memtime stamps) — and a row's byte offset is the tile's base plus a
 // compile-time row step times 4*ldo (no per-element multiply).  Rows >= M get
 // out-of-range buffer offsets: loads return 0, stores are dropped.
-template <int TM, int TN, int ACT, bool RB>
+template <int TM, int TN, int ACT, bool RB, bool CS = false>
 __device__ __forceinline__ void gemm_epilogue_store(const ConvGemmArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0,
-                                                    int wm, int wn, int lane) {
+                                                    int wm, int wn, int lane, double (*cs)[2] = nullptr) {
   const int r32 = lane & 31;
   const int h = lane >> 5;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
@@ -219,6 +219,14 @@ __device__ __forceinline__ void gemm_epilogue_store(const ConvGemmArgs& p, f32x1
       const int row0 = m0 + (wm * TM + i) * 32 + 4 * h;
       const int lim = p.M - row0;  // rows row0 + rr with rr < lim exist
       const int base = row0 * ldo4 + col * 4;
+      // CS: the 32-row tile lies wholly in the block's first utterance (0), wholly
+      // in the next one (1), or straddles the boundary / the end of M (2)
+      int mode = 2;
+      if constexpr (CS) {
+        const int t0 = m0 + (wm * TM + i) * 32;
+        const int next = (m0 / p.T + 1) * p.T;
+        if (t0 + 32 <= p.M) mode = t0 + 32 <= next ? 0 : (t0 >= next ? 1 : 2);
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rr = (r & 3) + 8 * (r >> 2);
@@ -235,14 +243,55 @@ __device__ __forceinline__ void gemm_epilogue_store(const ConvGemmArgs& p, f32x1
         y = y * sc + sh;
         const int off = rr < lim ? base + rr * ldo4 : kOOB;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, off, 0, 0);
+        if constexpr (CS) {  // rows < next: block's first utterance; next <= rows < M: the next one
+          const double yd = (double)y;
+          if (mode == 0) {
+            cs[j][0] += yd;
+          } else if (mode == 1) {
+            cs[j][1] += yd;
+          } else {
+            const int row = row0 + rr;
+            const int next = (m0 / p.T + 1) * p.T;
+            cs[j][0] += (row < next && row < p.M) ? yd : 0.0;
+            cs[j][1] += (row >= next && row < p.M) ? yd : 0.0;
+          }
+        }
       }
     }
   }
 }
 
-template <int TM, int TN>
+// Block-level reduction of the per-lane column sums into the f64 partials
+// p.colsum[((m0 / BM) * 2 + slot) * N + n] — lanes l and l+32 (same column) by
+// a shuffle, the WM waves of a column through LDS in wave order (fixed order:
+// deterministic).  All threads of the block call it (it holds a barrier); smem
+// must be free (after the k-loop's last barrier).
+template <int TN, int WM, int WN, int BM>
+__device__ __forceinline__ void gemm_colsum_reduce(const ConvGemmArgs& p, double (*cs)[2], int m0, int n0, int wm,
+                                                   int wn, int lane, unsigned char* smem) {
+  constexpr int BN = WN * TN * 32;
+  double* red = reinterpret_cast<double*>(smem);  // [WM][2][BN]
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const double v = cs[j][u] + __shfl_xor(cs[j][u], 32);
+      if (lane < 32) red[(wm * 2 + u) * BN + (wn * TN + j) * 32 + lane] = v;
+    }
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid < 2 * BN) {
+    const int u = tid / BN, c = tid - u * BN;
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) v += red[(w * 2 + u) * BN + c];
+    p.colsum[((size_t)(m0 / BM) * 2 + u) * p.N + n0 + c] = v;
+  }
+}
+
+template <int TM, int TN, int WM = 0, int WN = 0>
 __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0,
-                                              int wm, int wn, int lane) {
+                                              int wm, int wn, int lane, unsigned char* smem = nullptr) {
   const int r32 = lane & 31;
   const int h = lane >> 5;
   if (p.res) {
@@ -268,6 +317,21 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] += rv[j][r];
+    }
+  }
+  if constexpr (WM > 0) {
+    if (p.colsum) {  // fused per-utterance column sums (host: uniform batch, T >= BM, no row bias)
+      double cs[TN][2];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) cs[j][0] = cs[j][1] = 0.0;
+      switch (p.act) {
+        case kActRelu: gemm_epilogue_store<TM, TN, kActRelu, false, true>(p, acc, m0, n0, wm, wn, lane, cs); break;
+        case kActTanh: gemm_epilogue_store<TM, TN, kActTanh, false, true>(p, acc, m0, n0, wm, wn, lane, cs); break;
+        case kActGelu: gemm_epilogue_store<TM, TN, kActGelu, false, true>(p, acc, m0, n0, wm, wn, lane, cs); break;
+        default: gemm_epilogue_store<TM, TN, kActNone, false, true>(p, acc, m0, n0, wm, wn, lane, cs); break;
+      }
+      gemm_colsum_reduce<TN, WM, WN, WM * TM * 32>(p, cs, m0, n0, wm, wn, lane, smem);
+      return;
     }
   }
   if (p.row_bias) {

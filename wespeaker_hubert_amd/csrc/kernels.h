@@ -58,6 +58,11 @@ struct ConvGemmArgs {
   const int* seg;
   const int* iseg;
   int nseg;
+  // bf16x3 kernels, uniform batches with T >= block rows: per-utterance column
+  // sums of the epilogue output y, f64 partials [M / BM][2][N] (slot 0 = the
+  // utterance of the block's first row, 1 = the next); conv_gemm_colsum_mean()
+  // turns them into per-utterance means (the SE squeeze, ecapa_tdnn.py:118).
+  double* colsum;
 };
 
 // Fills the 1-D defaults (stride 1, Ti = T) of a zero-initialised ConvGemmArgs.
@@ -73,6 +78,13 @@ inline ConvGemmArgs normalized(ConvGemmArgs p) {
 // bf16 hi/lo images of W.  variant (N % 128 == 0): 0 = 128x128/4 waves,
 // 1 = 256x128/8 waves, 3 = 128x128 swizzled LDS rows (2 blocks/CU),
 // 4 = 256x128 swizzled LDS rows (default).
+// Rows per block of the bf16x3 tile launch_conv_gemm_x3 picks for p / variant
+// (the colsum partials' granularity).
+int conv_gemm_x3_block_rows(const ConvGemmArgs& p, int variant);
+// mean[b][n] = sum over the row blocks of utterance b of colsum partials / T
+// (fixed block order: the same sums whatever the batch), f32 out[b * ldo + n].
+void launch_colsum_mean(const double* part, int block_rows, int T, int B, int N, float* out, int ldo,
+                        hipStream_t s);
 void launch_conv_gemm_x3(const ConvGemmArgs& p, const void* whi, const void* wlo, int variant,
                          hipStream_t s);
 

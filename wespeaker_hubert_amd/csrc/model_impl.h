@@ -656,9 +656,10 @@ struct Model::Impl {
                             M * C, M * C, M * C,                   // h1..h3
                             (size_t)B * C, (size_t)B * 128, (size_t)B * C,  // gmean, ghid, gate
                             M * 1536, M * 128, M * 1536,           // xp, att, logit
-                            (size_t)B * 3072, (size_t)B * 128, (size_t)B * 3072};  // gstats, rowb, pooled
+                            (size_t)B * 3072, (size_t)B * 128, (size_t)B * 3072,  // gstats, rowb, pooled
+                            ((M + 127) / 128) * 2 * (size_t)C * 2};  // SE column-sum partials (f64)
     size_t o = 0;
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < 17; ++i) {
       if (offs) offs[i] = o;
       o += (sizes[i] + 63) / 64 * 64;  // 256-B alignment
     }
@@ -672,7 +673,7 @@ struct Model::Impl {
     const int M = seg ? M_seg : B * T, w = C / 8;
     cur_seg = seg;
     cur_nseg = B;
-    size_t off[16];
+    size_t off[17];
     ecapa_ws_floats(B, M, off);
     float* x[5] = {nullptr, ws + off[0], ws + off[1], ws + off[2], ws + off[3]};
     float* h1 = ws + off[4];
@@ -687,6 +688,11 @@ struct Model::Impl {
     float* gstats = ws + off[13];
     float* rowb = ws + off[14];
     float* pooled = ws + off[15];
+    double* sesum = reinterpret_cast<double*>(ws + off[16]);
+    // SE squeeze fused into conv3's epilogue (per-utterance f64 column sums) on the
+    // bf16x3 path for uniform batches whose utterances span >= one block of rows
+    const int se_bm = precision == 1 ? conv_gemm_x3_block_rows(ConvGemmArgs{.N = C}, x3_variant == 2 ? 4 : x3_variant) : 0;
+    const bool se_fused = precision == 1 && !seg && T >= se_bm;
 
     gemm("layer1", layer1, feats, feat_dim, x[1], C, M, T, 1, 2, kActRelu, s);
     for (int li = 0; li < 3; ++li) {
@@ -724,10 +730,12 @@ struct Model::Impl {
         g.cseg[2] = g.cseg[3] = C;
         fill(g, b.c3, M, T, 1, 0, h3, C, kActRelu, nullptr, true);
         g.role = 1;
+        if (se_fused) g.colsum = sesum;
         run("conv1x1_CxC", 2.0 * M * C * C, s, [&] { launch(g, b.c3, s); });
       }
       run("se", 0, s, [&] {
-        launch_frame_stats(h3, C, B, T, C, gmean, C, 0, 0, s, seg);
+        if (se_fused) launch_colsum_mean(sesum, se_bm, T, B, C, gmean, C, s);
+        else launch_frame_stats(h3, C, B, T, C, gmean, C, 0, 0, s, seg);
         launch_small_linear({gmean, C, b.se1.wt, b.se1.bias, ghid, 128, B, C, 128, 1}, s);
         launch_small_linear({ghid, 128, b.se2.wt, b.se2.bias, gate, C, B, 128, C, 3}, s);
         launch_residual_scale(xin, h3, gate, x[li + 2], B, T, C, s, seg, M);

@@ -121,14 +121,16 @@ __global__ __launch_bounds__(256) void frame_stats_kernel(const float* __restric
 }
 
 // Vector form (C, ldx multiples of 4): a lane owns 4 channels (16-B loads), a
-// wave every 4th frame, 4 frames in flight per lane with independent partial
-// sums — the scalar kernel keeps one dependent 4-B load per lane in flight.
+// wave every 4th frame, 4 frames in flight per lane.  Sums in f64: the mean is
+// then (up to rounding ties) the correctly rounded one whatever the summation
+// order, so it matches the fused conv3-epilogue SE sums (colsum partials) and a
+// utterance gets the same statistics in any batch.
 __global__ __launch_bounds__(256) void frame_stats4_kernel(const float* __restrict__ x, int ldx, int T_,
                                                            int C, float* __restrict__ out, int ldo,
                                                            int with_std, int std_off,
                                                            const int* __restrict__ seg) {
-  __shared__ f32x4 part[4][64];
-  __shared__ f32x4 s_mean[64];
+  __shared__ double part[4][4][64];
+  __shared__ float s_mean[4][64];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = (blockIdx.y * 64 + lane) * 4;
@@ -136,49 +138,58 @@ __global__ __launch_bounds__(256) void frame_stats4_kernel(const float* __restri
   const int T = seg ? seg[b + 1] - seg[b] : T_;
   const float* xb = x + (seg ? (long)seg[b] : (long)b * T_) * ldx + (ok ? c : 0);
   auto row = [&](int t) { return *reinterpret_cast<const f32x4*>(xb + (long)t * ldx); };
-  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  f32x4 s0 = z, s1 = z, s2 = z, s3 = z;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
   int t = wave;
   if (ok) {
     for (; t + 12 < T; t += 16) {
-      s0 += row(t);
-      s1 += row(t + 4);
-      s2 += row(t + 8);
-      s3 += row(t + 12);
+      const f32x4 r0 = row(t), r1 = row(t + 4), r2 = row(t + 8), r3 = row(t + 12);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] += ((double)r0[e] + (double)r1[e]) + ((double)r2[e] + (double)r3[e]);
     }
-    for (; t < T; t += 4) s0 += row(t);
+    for (; t < T; t += 4) {
+      const f32x4 r0 = row(t);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] += (double)r0[e];
+    }
   }
-  part[wave][lane] = (s0 + s1) + (s2 + s3);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) part[wave][e][lane] = a[e];
   __syncthreads();
-  const float inv = 1.f / (float)T;
   if (wave == 0) {
-    const f32x4 m = (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) * inv;
-    s_mean[lane] = m;
+    f32x4 m;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      m[e] = (float)((part[0][e][lane] + part[1][e][lane] + part[2][e][lane] + part[3][e][lane]) / (double)T);
+      s_mean[e][lane] = m[e];
+    }
     if (ok) *reinterpret_cast<f32x4*>(out + (long)b * ldo + c) = m;
   }
   __syncthreads();
   if (!with_std) return;
-  const f32x4 m = s_mean[lane];
-  f32x4 q0 = z, q1 = z;
-  t = wave;
-  if (ok) {
-    for (; t + 4 < T; t += 8) {
-      const f32x4 d0 = row(t) - m, d1 = row(t + 4) - m;
-      q0 += d0 * d0;
-      q1 += d1 * d1;
+  double q[4] = {0.0, 0.0, 0.0, 0.0};
+  float m[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) m[e] = s_mean[e][lane];
+  if (ok)
+    for (t = wave; t < T; t += 4) {
+      const f32x4 r0 = row(t);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const double d = (double)(r0[e] - m[e]);
+        q[e] += d * d;
+      }
     }
-    for (; t < T; t += 4) {
-      const f32x4 d = row(t) - m;
-      q0 += d * d;
-    }
-  }
   __syncthreads();
-  part[wave][lane] = q0 + q1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) part[wave][e][lane] = q[e];
   __syncthreads();
   if (wave == 0 && ok) {
-    const f32x4 v = (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) / (float)(T - 1);
     f32x4 r;
-    for (int e = 0; e < 4; ++e) r[e] = sqrtf(v[e] + 1e-7f);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const double v = (part[0][e][lane] + part[1][e][lane] + part[2][e][lane] + part[3][e][lane]) / (double)(T - 1);
+      r[e] = sqrtf((float)v + 1e-7f);
+    }
     float* o = out + (long)b * ldo + std_off + c;
     if (((ldo | std_off) & 3) == 0) *reinterpret_cast<f32x4*>(o) = r;
     else for (int e = 0; e < 4; ++e) o[e] = r[e];
