@@ -22,7 +22,7 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from wespeaker_hubert_amd.arch import (RESNET_ARCHS, ecapa_gflop_per_utt, hubert_gflop_per_utt,  # noqa: E402
+from wespeaker_hubert_amd.arch import (RESNET_ARCHS, ecapa_gflop_per_utt, hubert_gflop_per_utt, simam_gflop_per_utt,  # noqa: E402
                                        make_spec)
 from wespeaker_hubert_amd.frontend import compute_fbank  # noqa: E402
 from wespeaker_hubert_amd.s3prl_frontend import S3prlFrontend  # noqa: E402
@@ -42,7 +42,8 @@ DOMINANT_GEMM = {  # plain (role 0) 1-D GEMM: the HuBERT FFN fc1 (M = B*T, N = 3
 }
 HUBERT_ARCH = "HuBERT_ECAPA_GLOB_c512"  # C4: HuBERT-base front end + ECAPA_TDNN_GLOB_c512(feat_dim 768)
 HEAD_TAGS = ("layer1", "conv1x1_CxC", "res2_k3", "se", "conv_cat", "glob_ctx", "pool_linear1", "pool_linear2",
-             "astp", "head", "stem", "shortcut", "res_conv1x1", "res_conv3x3", "tstp_head")
+             "astp", "head", "stem", "shortcut", "res_conv1x1", "res_conv3x3", "tstp_head",
+             "simam", "asp_rows", "asp_linear1", "asp_linear2", "asp_pool_head")
 HUBERT_TAGS = ("h_conv0", "h_cnn", "h_ln", "h_proj", "h_pos_conv", "h_qkv", "h_attn", "h_out_proj", "h_fc1",
                "h_fc2", "h_cmn")
 
@@ -166,14 +167,17 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     hubert = args.arch == HUBERT_ARCH
-    B = args.batch or (64 if hubert else 128 if args.arch.startswith("ResNet") else 256)
+    simam = args.arch.startswith("SimAM")
+    resnet_like = args.arch.startswith("ResNet") or simam
+    B = args.batch or (64 if hubert else 128 if resnet_like else 256)
     N = int(round(args.seconds * 16000))
-    emb_dim = 256 if args.arch.startswith("ResNet") else 192
+    emb_dim = 256 if resnet_like else 192
     head_arch = "ECAPA_TDNN_GLOB_c512" if hubert else args.arch
     feat_dim = 768 if hubert else 80
-    spec = make_spec(head_arch, feat_dim=feat_dim, embed_dim=emb_dim)
-    model = HipSpeakerModel(head_arch, feat_dim=feat_dim, embed_dim=emb_dim)
-    sd = synth_state_dict(1234, model.state_dict_layout(), residual_tame=args.arch.startswith("ResNet"))
+    margs = dict(acoustic_dim=feat_dim, embed_dim=emb_dim) if simam else dict(feat_dim=feat_dim, embed_dim=emb_dim)
+    spec = make_spec(head_arch, **margs)
+    model = HipSpeakerModel(head_arch, **margs)
+    sd = synth_state_dict(1234, model.state_dict_layout(), residual_tame=resnet_like)
     model.load_state_dict(sd)
     fe, sd_fe = None, None
     if hubert:
@@ -244,7 +248,18 @@ def main():
                                 "tflops": round(fl / (avg * 1e-3) / 1e12, 2) if fl else None}
         k = kernels.get("h_fc1") if hubert else kernels.get("conv1x1_CxC")
         kr = kernels.get("res_conv1x1") if args.arch.startswith("ResNet") else None
-        if kr:
+        k3 = kernels.get("res_conv3x3") if simam else None
+        if k3:
+            # MFMA roofline of the SimAM-ResNet 3x3 convs as a class (all launches of a step)
+            ach = k3["tflops"] or 0.0
+            x3 = args.precision == 1
+            roof = {"kernel": "conv_gemm_x3 SimAM-ResNet 3x3 convs (res_conv3x3, all launches of a step)",
+                    "bound": "mfma", "achieved": ach, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": None, "traffic_source": None,
+                    "launches_per_step": k3["launches_per_step"], "ms_per_step": k3["ms_per_step"],
+                    "mfma_dtype": "bf16 (3-term split, fp32 accumulate)", "mfma_work_factor": 3 if x3 else 1,
+                    "frac_of_issue_peak": round(ach * 3 / BF16_MFMA_PEAK_TFLOPS, 4)}
+        elif kr:
             # HBM roofline of the ResNet 1x1 convs as a class (all launches of a step)
             byts = resnet_1x1_bytes_per_utt(args.arch, 80, T) * B
             ach = byts / (kr["ms_per_step"] * 1e-3) / 1e9
@@ -290,7 +305,7 @@ def main():
                     "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4)}
 
     gf = hubert_gflop_per_utt(N) + ecapa_gflop_per_utt(spec, T) if hubert else ecapa_gflop_per_utt(spec, T) \
-        if args.arch.startswith("ECAPA") else sum(
+        if args.arch.startswith("ECAPA") else simam_gflop_per_utt(spec, T) if simam else sum(
         v["ms_per_step"] * (v["tflops"] or 0) for v in kernels.values()) / B if kernels else 0.0
     res = {
         "metric": "embeddings/sec on 5s 16kHz utts",

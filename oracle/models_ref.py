@@ -160,8 +160,55 @@ def resnet_forward(feats: Tensor, sd: Dict[str, Tensor], arch: str, two_emb_laye
     return torch.tensor(0.0), e
 
 
+# ------------------------------------------------------------ SimAM-ResNet ---
+SIMAM_BLOCKS = {"SimAM_ResNet34_ASP": [3, 4, 6, 3], "SimAM_ResNet100_ASP": [6, 16, 24, 3]}
+
+
+def _simam(x: Tensor, lam: float = 1e-4) -> Tensor:
+    """SimAMBasicBlock.SimAM — samresnet.py:64-69: energy over the F*T positions,
+    variance with the (n - 1) divisor."""
+    n = x.shape[2] * x.shape[3] - 1
+    d = (x - x.mean(dim=(2, 3), keepdim=True)) ** 2
+    v = d.sum(dim=(2, 3), keepdim=True) / n
+    return x * torch.sigmoid(d / (4 * (v + lam)) + 0.5)
+
+
+def _simam_block(x, sd, p, stride):
+    """SimAMBasicBlock.forward — samresnet.py:56-62."""
+    out = F.relu(_bn(F.conv2d(x, sd[p + ".conv1.weight"], stride=stride, padding=1), sd, p + ".bn1"))
+    out = _simam(_bn(F.conv2d(out, sd[p + ".conv2.weight"], padding=1), sd, p + ".bn2"))
+    sc = x
+    if (p + ".downsample.0.weight") in sd:
+        sc = _bn(F.conv2d(x, sd[p + ".downsample.0.weight"], stride=stride), sd, p + ".downsample.1")
+    return F.relu(out + sc)
+
+
+def asp(x: Tensor, sd: Dict[str, Tensor], p: str) -> Tensor:
+    """ASP.forward — pooling_layers.py:166-173: (B,C,F,T) -> (B,C*F,T), attention
+    Conv1d -> ReLU -> BN -> Conv1d -> softmax over T, clamp 1e-5."""
+    x = x.reshape(x.shape[0], -1, x.shape[-1])
+    h = _bn(F.relu(F.conv1d(x, sd[p + ".0.weight"], sd[p + ".0.bias"])), sd, p + ".2")
+    w = torch.softmax(F.conv1d(h, sd[p + ".3.weight"], sd[p + ".3.bias"]), dim=2)
+    mu = torch.sum(x * w, dim=2)
+    sg = torch.sqrt((torch.sum(x * x * w, dim=2) - mu * mu).clamp(min=1e-5))
+    return torch.cat((mu, sg), 1)
+
+
+def simam_forward(feats: Tensor, sd: Dict[str, Tensor], arch: str) -> Tensor:
+    """SimAM_ResNet*_ASP.forward — samresnet.py:135-143 (returns the embedding)."""
+    x = feats.permute(0, 2, 1).unsqueeze(1)
+    out = F.relu(_bn(F.conv2d(x, sd["front.conv1.weight"], padding=1), sd, "front.bn1"))
+    for li, n in enumerate(SIMAM_BLOCKS[arch]):
+        for bi in range(n):
+            stride = 2 if (li > 0 and bi == 0) else 1
+            out = _simam_block(out, sd, f"front.layer{li + 1}.{bi}", stride)
+    return F.linear(asp(out, sd, "pooling.attention"), sd["bottleneck.weight"], sd["bottleneck.bias"])
+
+
 def forward(arch: str, feats: Tensor, sd: Dict[str, Tensor], emb_bn: bool = False):
-    """Registry dispatch — speaker_model.py:30-57 (prefix match)."""
+    """Registry dispatch — speaker_model.py:30-57 (prefix match).  Always (aux, embed)."""
+    if arch.startswith("SimAM_ResNet"):
+        return None, simam_forward(feats, sd, arch)
     if arch.startswith("ECAPA_TDNN"):
         return ecapa_forward(feats, sd, glob="GLOB" in arch, emb_bn=emb_bn)
     if arch.startswith("ResNet"):

@@ -49,7 +49,8 @@ def _import_reference():
     for stub in ("fire", "kaldiio", "onnxruntime"):
         if stub not in sys.modules:
             sys.modules[stub] = types.ModuleType(stub)
-    from wespeaker.models import ecapa_tdnn, pooling_layers, resnet  # noqa
+    from wespeaker.models import ecapa_tdnn, pooling_layers, resnet, samresnet  # noqa
+    _import_reference.samresnet = samresnet
     from wespeaker.bin import score_norm  # noqa
     from wespeaker.utils import score_metrics  # noqa
     return ecapa_tdnn, resnet, pooling_layers, score_norm, score_metrics
@@ -75,16 +76,25 @@ MODEL_CASES = [
     ("ecapa_glob_c512_ssl768_b2_t250", "ECAPA_TDNN_GLOB_c512", dict(feat_dim=768, embed_dim=192), 16, 107, 2, 250, False),
     ("resnet34_b2_t200", "ResNet34", dict(feat_dim=80, embed_dim=256), 21, 201, 2, 200, True),
     ("resnet293_b1_t160", "ResNet293", dict(feat_dim=80, embed_dim=256), 22, 202, 1, 160, True),
+    # samresnet.py:124-166 (hub "vblinkp"/"vblinkf" backbone); ctor takes acoustic_dim
+    ("simam34_b2_t200", "SimAM_ResNet34_ASP", dict(acoustic_dim=80, embed_dim=256), 31, 301, 2, 200, True),
+    ("simam34_inpl32_b1_t97", "SimAM_ResNet34_ASP", dict(in_planes=32, acoustic_dim=40, embed_dim=128),
+     32, 302, 1, 97, True),
+    ("simam100_b1_t123", "SimAM_ResNet100_ASP", dict(acoustic_dim=80, embed_dim=256), 33, 303, 1, 123, True),
 ]
 
 
-def make_models(out):
+def make_models(out, only=None):
     ecapa_tdnn, resnet, _, _, _ = _import_reference()
     for name, ctor, kw, wseed, iseed, B, T, tame in MODEL_CASES:
-        mod = ecapa_tdnn if ctor.startswith("ECAPA") else resnet
+        if only and not any(o in name for o in only):
+            continue
+        mod = ecapa_tdnn if ctor.startswith("ECAPA") else (
+            _import_reference.samresnet if ctor.startswith("SimAM") else resnet)
         torch.manual_seed(0)
         model = load_synth(getattr(mod, ctor)(**kw), wseed, residual_tame=tame)
-        x = synth_feats(iseed, B, T, kw["feat_dim"])
+        feat_dim = kw.get("feat_dim", kw.get("acoustic_dim"))
+        x = synth_feats(iseed, B, T, feat_dim)
         inter = {}
         hooks = []
         if name == "ecapa_c512_b2_t200":
@@ -98,7 +108,8 @@ def make_models(out):
         for h in hooks:
             h.remove()
         rec = dict(arch=np.array(ctor), weight_seed=np.int64(wseed), input_seed=np.int64(iseed),
-                   B=np.int64(B), T=np.int64(T), feat_dim=np.int64(kw["feat_dim"]),
+                   B=np.int64(B), T=np.int64(T), feat_dim=np.int64(feat_dim),
+                   in_planes=np.int64(kw.get("in_planes", 64 if ctor.startswith("SimAM") else 32)),
                    embed_dim=np.int64(kw["embed_dim"]), emb_bn=np.int64(int(kw.get("emb_bn", False))),
                    residual_tame=np.int64(int(tame)),
                    input_sum=np.float64(x.astype(np.float64).sum()), input_head=x.reshape(-1)[:16].copy(),
@@ -191,14 +202,61 @@ def make_scoring(out):
     print("scoring eer", eer, "mindcf", mindcf)
 
 
+def make_calibration(out):
+    """bin/score_calibration.py:30-164 (gather -> train -> infer) on a synthetic
+    AS-Norm side-output file; stores the inputs, the factor lines, the fitted
+    weights and the calibrated scores."""
+    import importlib
+    import tempfile
+    _import_reference()
+    cal = importlib.import_module("wespeaker.bin.score_calibration")
+    for stub in ("fire", "kaldiio", "onnxruntime"):  # torch.optim probes module specs: drop the stubs
+        if getattr(sys.modules.get(stub), "__spec__", 0) is None:
+            del sys.modules[stub]
+    rng = np.random.default_rng(501)
+    n_utt, n_trial = 40, 600
+    utts = [f"id{i // 4:03d}/u{i:03d}.wav" for i in range(n_utt)]
+    dur = rng.uniform(2.0, 20.0, n_utt)
+    mag = rng.uniform(8.0, 14.0, n_utt)
+    cmean = rng.uniform(0.05, 0.3, n_utt)
+    a = rng.integers(0, n_utt, n_trial)
+    b = (a + 1 + rng.integers(0, n_utt - 1, n_trial)) % n_utt
+    tgt = (a // 4) == (b // 4)
+    score = np.where(tgt, rng.normal(3.0, 1.2, n_trial), rng.normal(-0.5, 1.0, n_trial))
+    with tempfile.TemporaryDirectory() as d:
+        dur_scp, sn, fac = os.path.join(d, "dur"), os.path.join(d, "sn"), os.path.join(d, "fac")
+        mdl, cs = os.path.join(d, "m.pt"), os.path.join(d, "cal")
+        with open(dur_scp, "w") as f:
+            for u, t in zip(utts, dur):
+                f.write(f"{u} {t:.3f}\n")
+        with open(sn, "w") as f:
+            for i in range(n_trial):
+                f.write("{} {} {:.5f} {} {:.4f} {:.4f} {:.4f} {:.4f}\n".format(
+                    utts[a[i]], utts[b[i]], score[i], "target" if tgt[i] else "nontarget",
+                    mag[a[i]], mag[b[i]], cmean[a[i]], cmean[b[i]]))
+        cal.gather_calibration_factors(dur_scp, 15.0, sn, fac)
+        cal.train_calibration_model(fac, mdl)
+        cal.infer_calibration(fac, mdl, cs)
+        sd = torch.load(mdl, weights_only=True)
+        res = dict(dur_lines=np.array(open(dur_scp).read().splitlines()),
+                   score_norm_lines=np.array(open(sn).read().splitlines()),
+                   factor_lines=np.array(open(fac).read().splitlines()),
+                   weight=sd["linear.weight"].numpy(), bias=sd["linear.bias"].numpy(),
+                   calibrated_lines=np.array(open(cs).read().splitlines()), max_dur=np.float64(15.0))
+    np.savez_compressed(os.path.join(out, "calibration.npz"), **res)
+    print("calibration weight", res["weight"], "bias", res["bias"])
+
+
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 1)
-    what = sys.argv[1:] or ["models", "pooling", "scoring", "diar"]
+    what = sys.argv[1:] or ["models", "pooling", "scoring", "diar", "calibration"]
+    if "calibration" in what:
+        make_calibration(HERE)
     if "pooling" in what:
         make_pooling(HERE)
     if "scoring" in what:
         make_scoring(HERE)
     if "diar" in what:
         make_diar(HERE)
-    if "models" in what:
-        make_models(HERE)
+    if "models" in what:  # `models simam` regenerates only the fixtures whose name contains "simam"
+        make_models(HERE, [w for w in what if w not in ("models", "pooling", "scoring", "diar", "calibration")])

@@ -21,6 +21,7 @@ from wespeaker_hubert_amd.synthetic import synth_audio, synth_feats, synth_state
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 ECAPA_FIX = sorted(p for p in glob.glob(os.path.join(GOLD, "ecapa*.npz")))
 RESNET_FIX = sorted(p for p in glob.glob(os.path.join(GOLD, "resnet*.npz")))
+SIMAM_FIX = sorted(p for p in glob.glob(os.path.join(GOLD, "simam*.npz")))
 EMB_ATOL = 1e-4
 EMB_COS = 0.9999
 
@@ -105,6 +106,38 @@ def test_resnet_matches_oracle(arch, B, T):
     with torch.no_grad():
         _, ref = models_ref.forward(arch, torch.from_numpy(x), {k: torch.from_numpy(v) for k, v in sd.items()})
     _assert_emb(emb.cpu().numpy(), ref.numpy())
+
+
+@pytest.mark.parametrize("path", SIMAM_FIX, ids=[os.path.basename(p)[:-4] for p in SIMAM_FIX])
+def test_simam_matches_reference_fixture(path):
+    """SimAM_ResNet{34,100}_ASP (samresnet.py) vs the reference module's own outputs."""
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    z = np.load(path, allow_pickle=False)
+    m = HipSpeakerModel(str(z["arch"]), in_planes=int(z["in_planes"]), acoustic_dim=int(z["feat_dim"]),
+                        embed_dim=int(z["embed_dim"]))
+    m.load_state_dict(synth_state_dict(int(z["weight_seed"]), m.state_dict_layout(), residual_tame=True))
+    m.to(DEV)
+    x = synth_feats(int(z["input_seed"]), int(z["B"]), int(z["T"]), int(z["feat_dim"]))
+    emb = m(torch.from_numpy(x).to(DEV))  # the module returns the embedding itself
+    assert isinstance(emb, torch.Tensor)
+    _assert_emb(emb.cpu().numpy(), z["embed"])
+
+
+@pytest.mark.parametrize("arch,B,T", [("SimAM_ResNet34_ASP", 3, 301), ("SimAM_ResNet34_ASP", 2, 9),
+                                      ("SimAM_ResNet100_ASP", 2, 64)])
+def test_simam_matches_oracle(arch, B, T):
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    m = HipSpeakerModel(arch, acoustic_dim=80, embed_dim=256)
+    sd = synth_state_dict(19, m.state_dict_layout(), residual_tame=True)
+    m.load_state_dict(sd)
+    m.to(DEV)
+    x = synth_feats(97, B, T, 80)
+    emb = m(torch.from_numpy(x).to(DEV))
+    with torch.no_grad():
+        _, ref = models_ref.forward(arch, torch.from_numpy(x), {k: torch.from_numpy(v) for k, v in sd.items()})
+    _assert_emb(emb.cpu().numpy(), ref.numpy())
+    e0 = m(torch.from_numpy(x[1:2]).to(DEV))  # batch independence
+    assert np.abs(e0.cpu().numpy() - emb[1:2].cpu().numpy()).max() < 1e-5
 
 
 def test_ecapa_deterministic():

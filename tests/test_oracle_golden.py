@@ -13,14 +13,18 @@ from wespeaker_hubert_amd.synthetic import synth_feats, synth_state_dict
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 MODEL_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLD, "*.npz"))
-                        if os.path.basename(p).startswith(("ecapa", "resnet")))
+                        if os.path.basename(p).startswith(("ecapa", "resnet", "simam")))
 
 
 def load_case(path):
     z = np.load(path, allow_pickle=False)
     arch = str(z["arch"])
-    spec = A.make_spec(arch, feat_dim=int(z["feat_dim"]), embed_dim=int(z["embed_dim"]),
-                       emb_bn=bool(int(z["emb_bn"])))
+    if arch.startswith("SimAM"):  # SimAM_ResNet*_ASP(in_planes, embed_dim, acoustic_dim)
+        spec = A.make_spec(arch, in_planes=int(z["in_planes"]), acoustic_dim=int(z["feat_dim"]),
+                           embed_dim=int(z["embed_dim"]))
+    else:
+        spec = A.make_spec(arch, feat_dim=int(z["feat_dim"]), embed_dim=int(z["embed_dim"]),
+                           emb_bn=bool(int(z["emb_bn"])))
     plist = A.param_list(spec)
     sd = synth_state_dict(int(z["weight_seed"]), plist, residual_tame=bool(int(z["residual_tame"])))
     x = synth_feats(int(z["input_seed"]), int(z["B"]), int(z["T"]), int(z["feat_dim"]))

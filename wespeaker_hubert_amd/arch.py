@@ -31,6 +31,12 @@ RESNET_ARCHS = {
     "ResNet293": ("bottleneck", (10, 20, 64, 3)),
 }
 
+SIMAM_ARCHS = {
+    # name: num_blocks of SimAMBasicBlock — samresnet.py:115-121, 124-166
+    "SimAM_ResNet34_ASP": (3, 4, 6, 3),
+    "SimAM_ResNet100_ASP": (6, 16, 24, 3),
+}
+
 
 @dataclass
 class ModelSpec:
@@ -49,6 +55,8 @@ class ModelSpec:
             return "ecapa"
         if self.arch.startswith("ResNet"):
             return "resnet"
+        if self.arch.startswith("SimAM_ResNet"):
+            return "simam"
         raise KeyError(self.arch)
 
 
@@ -57,9 +65,18 @@ def make_spec(arch: str, **model_args) -> ModelSpec:
 
     Unknown names raise (the reference prints and exit(1)s, speaker_model.py:55-57).
     """
-    if arch not in ECAPA_ARCHS and arch not in RESNET_ARCHS:
-        raise KeyError(f"{arch} not found !!! (supported: {sorted(ECAPA_ARCHS) + sorted(RESNET_ARCHS)})")
+    if arch not in ECAPA_ARCHS and arch not in RESNET_ARCHS and arch not in SIMAM_ARCHS:
+        raise KeyError(f"{arch} not found !!! (supported: "
+                       f"{sorted(ECAPA_ARCHS) + sorted(RESNET_ARCHS) + sorted(SIMAM_ARCHS)})")
     kw = dict(model_args)
+    if arch in SIMAM_ARCHS:
+        # SimAM_ResNet*_ASP(in_planes=64, embed_dim=256, acoustic_dim=80, dropout=0)
+        spec = ModelSpec(arch=arch, feat_dim=int(kw.pop("acoustic_dim", 80)),
+                         embed_dim=int(kw.pop("embed_dim", 256)), pooling_func="ASP",
+                         m_channels=int(kw.pop("in_planes", 64)))
+        kw.pop("dropout", None)  # eval: nn.Dropout is the identity
+        spec.extra = kw
+        return spec
     spec = ModelSpec(arch=arch,
                      feat_dim=int(kw.pop("feat_dim", 80 if arch.startswith("ECAPA") else 40)),
                      embed_dim=int(kw.pop("embed_dim", 192 if arch.startswith("ECAPA") else 128)),
@@ -137,8 +154,54 @@ def resnet_params(spec: ModelSpec) -> ParamList:
     return out
 
 
+def simam_params(spec: ModelSpec) -> ParamList:
+    """state_dict layout of SimAM_ResNet*_ASP (samresnet.py:72-166, ASP pooling_layers.py:151-164)."""
+    m = spec.m_channels
+    out: ParamList = [("front.conv1.weight", (m, 1, 3, 3))] + _bn("front.bn1", m)
+    in_planes = m
+    for li, n in enumerate(SIMAM_ARCHS[spec.arch]):
+        planes = m * (2 ** li)
+        for bi in range(n):
+            stride = 2 if (li > 0 and bi == 0) else 1
+            p = f"front.layer{li + 1}.{bi}"
+            out += [(p + ".conv1.weight", (planes, in_planes, 3, 3))] + _bn(p + ".bn1", planes)
+            out += [(p + ".conv2.weight", (planes, planes, 3, 3))] + _bn(p + ".bn2", planes)
+            if stride != 1 or in_planes != planes:
+                out += [(p + ".downsample.0.weight", (planes, in_planes, 1, 1))] + _bn(p + ".downsample.1", planes)
+            in_planes = planes
+    cf = m * 8 * int(spec.feat_dim / 8)
+    out += [("pooling.attention.0.weight", (128, cf, 1)), ("pooling.attention.0.bias", (128,))]
+    out += _bn("pooling.attention.2", 128)
+    out += [("pooling.attention.3.weight", (cf, 128, 1)), ("pooling.attention.3.bias", (cf,))]
+    out += [("bottleneck.weight", (spec.embed_dim, 2 * cf)), ("bottleneck.bias", (spec.embed_dim,))]
+    return out
+
+
 def param_list(spec: ModelSpec) -> ParamList:
-    return ecapa_params(spec) if spec.family == "ecapa" else resnet_params(spec)
+    if spec.family == "ecapa":
+        return ecapa_params(spec)
+    if spec.family == "simam":
+        return simam_params(spec)
+    return resnet_params(spec)
+
+
+def simam_gflop_per_utt(spec: ModelSpec, T: int) -> float:
+    """Algorithmic FLOPs (2 x MACs) of one SimAM-ResNet forward over T frames."""
+    m, F, t = spec.m_channels, spec.feat_dim, T
+    macs = F * t * m * 9  # stem
+    cin = m
+    for li, n in enumerate(SIMAM_ARCHS[spec.arch]):
+        planes = m * (2 ** li)
+        for bi in range(n):
+            stride = 2 if (li > 0 and bi == 0) else 1
+            Fo, To = (F - 1) // stride + 1, (t - 1) // stride + 1
+            macs += Fo * To * planes * (cin * 9 + planes * 9)
+            if stride != 1 or cin != planes:
+                macs += Fo * To * planes * cin
+            F, t, cin = Fo, To, planes
+    cf = cin * F
+    macs += t * (cf * 128 * 2) + 2 * cf * spec.embed_dim
+    return 2.0 * macs / 1e9
 
 
 def ecapa_gflop_per_utt(spec: ModelSpec, T: int) -> float:

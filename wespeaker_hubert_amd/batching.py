@@ -69,7 +69,9 @@ def embed_utterances(model, pcms: Sequence, device, max_frames: int = DEFAULT_MA
     if not getattr(model, "supports_segments", False):
         for x in pcms:  # ResNet: per-utterance forward
             feats = compute_fbank(torch.as_tensor(np.asarray(x, np.float32)).to(device)[None], scale=scale, cmn=True)
-            out.append(model(feats)[-1][0].cpu().numpy())
+            outputs = model(feats)
+            outputs = outputs[-1] if isinstance(outputs, tuple) else outputs
+            out.append(outputs[0].cpu().numpy())
         return out
     for lo, hi in pack([len(x) for x in pcms], max_frames):
         wav = [torch.from_numpy(np.asarray(x, np.float32)) for x in pcms[lo:hi]]

@@ -186,7 +186,8 @@ def extract(config="conf/config.yaml", **kwargs):
             feats = compute_fbank(x, scale=1.0, cmn=True)
         else:  # torchaudio.load(normalize=True) audio in [-1, 1]; apply_cmvn fused
             feats = frontend.extract(x * (1.0 / 32768.0), cmn=True)
-        emb = model(feats)[-1].cpu().numpy()
+        outputs = model(feats)  # extract.py:114-116: embed or (aux, embed)
+        emb = (outputs[-1] if isinstance(outputs, tuple) else outputs).cpu().numpy()
         for k, e in zip(keys, emb):
             writer(k, e)
 

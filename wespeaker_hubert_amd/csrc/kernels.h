@@ -128,9 +128,20 @@ void launch_residual_scale(const float* x, const float* h, const float* g, float
                            int T, int C, hipStream_t s, const int* seg = nullptr, int M = 0);
 
 // ASTP attentive statistics (pooling_layers.py:135-144): softmax over frames
-// of logits e [rows][C], weighted mean/std of x [rows][C] -> out [B][2C].
+// of logits e [rows][C], weighted mean/std of x [rows][C] -> out [B][2C];
+// std = sqrt(clamp(E[x^2] - mu^2, var_floor)) (1e-7 ASTP, 1e-5 ASP pooling_layers.py:170).
 void launch_astp_pool(const float* e, const float* x, int B, int T, int C, float* out,
-                      hipStream_t s, const int* seg = nullptr);
+                      hipStream_t s, const int* seg = nullptr, float var_floor = 1e-7f);
+
+// SimAM attention + shortcut + ReLU of a SimAMBasicBlock (samresnet.py:56-69):
+// out = relu(z * sigmoid((z - mean)^2 / (4 (var_{n-1} + 1e-4)) + 0.5) + res), statistics
+// per (utterance, channel) over the `rows` = F*T positions of z [B][rows][C] (NHWC).
+// part: f64 scratch [B][simam_chunks(B, rows)][2][C]; coef: f32 scratch [B][2][C].
+int simam_chunks(int B, int rows);
+void launch_simam(const float* z, const float* res, float* out, int B, int rows, int C, double* part, float* coef,
+                  hipStream_t s);
+// [B][F][T][C] -> [B][T][F][C]: ASP's x.reshape(B, C*F, T) as frame rows (channel order f*C + c).
+void launch_nhwc_to_tfc(const float* in, float* out, int B, int F, int T, int C, hipStream_t s);
 
 // ResNet stem: 1 -> C0 3x3 conv + folded BN + ReLU, (B,T,F) feats -> NHWC [B][F][T][C0].
 void launch_resnet_stem(const float* feats, int B, int T, int F, int C0, const float* w, const float* bias,

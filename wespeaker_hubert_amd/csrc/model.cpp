@@ -62,6 +62,20 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
     m.bottleneck = it->second.first;
     for (int i = 0; i < 4; ++i) m.nblocks[i] = it->second.second[i];
     m.build_resnet_params();
+  } else if (arch == "SimAM_ResNet34_ASP" || arch == "SimAM_ResNet100_ASP") {
+    // samresnet.py:124-166: in_planes 64 (option "in_planes" before the weights),
+    // acoustic_dim = feat_dim, basic SimAM blocks [3,4,6,3] / [6,16,24,3]
+    WSP_CHECK(!two_emb && !emb_bn, "SimAM-ResNet has no emb_bn / two_emb_layer");
+    WSP_CHECK(feat_dim >= 8 && feat_dim % 8 == 0, "SimAM-ResNet acoustic_dim must be a multiple of 8");
+    WSP_CHECK(embed_dim > 0, "embed_dim must be positive");
+    m.ecapa = false;
+    m.simam = true;
+    m.bottleneck = false;
+    m.x3_variant = 3;
+    m.m_ch = 64;
+    const int nb34[4] = {3, 4, 6, 3}, nb100[4] = {6, 16, 24, 3};
+    for (int i = 0; i < 4; ++i) m.nblocks[i] = arch == "SimAM_ResNet34_ASP" ? nb34[i] : nb100[i];
+    m.build_simam_params();
   } else if (arch == "HuBERT_base") {
     // s3prl HuBERT-base upstream + Featurizer (frontend/s3prl.py); input is
     // the waveform, output 768-dim frames (S3prlFrontend.output_size()).
@@ -105,6 +119,8 @@ void Model::finalize() {
               "parameter not set: " + p.name);
   if (m.ecapa)
     m.finalize_ecapa();
+  else if (m.simam)
+    m.finalize_simam();
   else if (m.hubert)
     m.finalize_hubert();
   else
@@ -118,8 +134,9 @@ int Model::feat_dim() const { return impl->feat_dim; }
 
 size_t Model::workspace_bytes(int B, int T) const {
   WSP_CHECK(!impl->hubert, "HuBERT handle: use the front-end workspace query");
-  const size_t f = impl->ecapa ? impl->ecapa_ws_floats(B, (size_t)B * T, nullptr)
-                               : impl->resnet_ws_floats(B, T, nullptr);
+  const size_t f = impl->ecapa   ? impl->ecapa_ws_floats(B, (size_t)B * T, nullptr)
+                   : impl->simam ? impl->simam_ws_floats(B, T, nullptr)
+                                 : impl->resnet_ws_floats(B, T, nullptr);
   return f * sizeof(float) + 256;
 }
 
@@ -136,7 +153,12 @@ void Model::forward(const float* feats, int B, int T, float* embed, void* ws, si
     m.forward_ecapa(feats, B, T, embed, wsf, s);
   } else {
     WSP_CHECK(m.precision == 1, "ResNet runs on the bf16x3 kernels only (precision=1)");
-    m.forward_resnet(feats, B, T, embed, wsf, s);
+    if (m.simam) {
+      WSP_CHECK((T + 7) / 8 >= 2, "SimAM-ResNet needs >= 2 frames after the three stride-2 stages");
+      m.forward_simam(feats, B, T, embed, wsf, s);
+    } else {
+      m.forward_resnet(feats, B, T, embed, wsf, s);
+    }
   }
 }
 
@@ -169,6 +191,13 @@ void Model::set_option(const std::string& key, int value) {
     WSP_CHECK(!impl->finalized, "option 'layer' must be set before finalize");
     WSP_CHECK(value >= -1 && value <= 12, "layer must be -1 (weighted sum) or 0..12");
     impl->h_layer_sel = value;
+  } else if (key == "in_planes") {
+    WSP_CHECK(impl->simam, "option 'in_planes' applies to SimAM-ResNet handles");
+    WSP_CHECK(!impl->finalized, "option 'in_planes' must be set before finalize");
+    WSP_CHECK(value == 32 || value == 64, "in_planes must be 32 or 64");
+    for (const auto& p : impl->params) WSP_CHECK(!p.set, "option 'in_planes' must be set before the weights");
+    impl->m_ch = value;
+    impl->build_simam_params();
   } else if (key == "x3_variant") {
     WSP_CHECK(value >= 0 && value <= 4, "x3_variant must be 0..4");
     impl->x3_variant = value;

@@ -151,6 +151,12 @@ struct Model::Impl {
   std::vector<RBlock> rblocks;
   LinW seg1;
 
+  // SimAM-ResNet (samresnet.py:20-166): basic blocks whose bn2 output passes
+  // SimAM before the shortcut add, ASP pooling, `bottleneck` Linear.
+  bool simam = false;
+  ConvW asp1, asp2;
+  LinW simam_head;
+
   // HuBERT-base front end (hubert_model.cpp), channels-last [B][T][C]
   bool hubert = false;
   float* h_conv0_w = nullptr;  // [512][10]
@@ -527,6 +533,175 @@ struct Model::Impl {
         launch_frame_stats(x, Ci, nb * Fi, Ti, Ci, pooled, 2 * Ci, 1, Ci, s);
         launch_small_linear({pooled, Fi * 2 * Ci, seg1.wt, seg1.bias, embed + (size_t)b0 * embed_dim, embed_dim, nb,
                              Fi * 2 * Ci, embed_dim, 0},
+                            s);
+      });
+    }
+  }
+
+  // ------------------------------------------------------------ SimAM ---
+  // state_dict of SimAM_ResNet{34,100}_ASP (samresnet.py:72-166): front.* backbone,
+  // pooling.attention.{0,2,3} (ASP, pooling_layers.py:151-173), bottleneck.
+  void build_simam_params() {
+    params.clear();
+    idx.clear();
+    rblocks.clear();
+    add("front.conv1.weight", {m_ch, 1, 3, 3});
+    add_bn("front.bn1", m_ch);
+    int in_planes = m_ch;
+    for (int li = 0; li < 4; ++li) {
+      const int planes = m_ch << li;
+      for (int bi = 0; bi < nblocks[li]; ++bi) {
+        const int stride = (li > 0 && bi == 0) ? 2 : 1;
+        const std::string p = "front.layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+        RBlock rb;
+        rb.stride = stride;
+        rb.in_planes = in_planes;
+        rb.planes = planes;
+        rb.out_planes = planes;
+        add(p + ".conv1.weight", {planes, in_planes, 3, 3});
+        add_bn(p + ".bn1", planes);
+        add(p + ".conv2.weight", {planes, planes, 3, 3});
+        add_bn(p + ".bn2", planes);
+        if (stride != 1 || in_planes != planes) {
+          rb.has_sc = true;
+          add(p + ".downsample.0.weight", {planes, in_planes, 1, 1});
+          add_bn(p + ".downsample.1", planes);
+        }
+        rblocks.push_back(rb);
+        in_planes = planes;
+      }
+    }
+    const int CF = 8 * m_ch * (feat_dim / 8);  // ASP: in_planes * 8 * int(acoustic_dim / 8)
+    add("pooling.attention.0.weight", {128, CF, 1});
+    add("pooling.attention.0.bias", {128});
+    add_bn("pooling.attention.2", 128);
+    add("pooling.attention.3.weight", {CF, 128, 1});
+    add("pooling.attention.3.bias", {CF});
+    add("bottleneck.weight", {embed_dim, 2 * CF});
+    add("bottleneck.bias", {embed_dim});
+  }
+
+  void finalize_simam() {
+    {
+      std::vector<double> sc, sh;
+      bn_affine("front.bn1", sc, sh);
+      const auto& w = P("front.conv1.weight");
+      std::vector<float> wf(m_ch * 9), bf(m_ch);
+      for (int c = 0; c < m_ch; ++c) {
+        for (int q = 0; q < 9; ++q) wf[c * 9 + q] = (float)(w[c * 9 + q] * sc[c]);
+        bf[c] = (float)sh[c];
+      }
+      stem_w = dev.upload(wf);
+      stem_b = dev.upload(bf);
+    }
+    int ib = 0;
+    for (int li = 0; li < 4; ++li)
+      for (int bi = 0; bi < nblocks[li]; ++bi) {
+        RBlock& rb = rblocks[ib++];
+        const std::string p = "front.layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+        rb.c1 = pack_conv_bn(p + ".conv1.weight", p + ".bn1", rb.planes, rb.in_planes, 9);
+        rb.c2 = pack_conv_bn(p + ".conv2.weight", p + ".bn2", rb.planes, rb.planes, 9);
+        if (rb.has_sc)
+          rb.sc = pack_conv_bn(p + ".downsample.0.weight", p + ".downsample.1", rb.planes, rb.in_planes, 1);
+      }
+    // reference channel index c*F4 + f of x.reshape(B, C*F, T); ours f*C4 + c (frame rows [T][F][C])
+    const int C4 = rblocks.back().out_planes, F4 = feat_dim / 8, CF = C4 * F4;
+    auto ref_ch = [&](int k) { return (k % C4) * F4 + k / C4; };
+    {
+      const auto& W = P("pooling.attention.0.weight");
+      std::vector<float> wp((size_t)128 * CF);
+      for (int n = 0; n < 128; ++n)
+        for (int k = 0; k < CF; ++k) wp[(size_t)n * CF + k] = W[(size_t)n * CF + ref_ch(k)];
+      asp1 = pack_conv(wp, 128, CF, 1, P("pooling.attention.0.bias").data(), "pooling.attention.2");
+    }
+    {
+      const auto& W = P("pooling.attention.3.weight");
+      const auto& bb = P("pooling.attention.3.bias");
+      std::vector<float> wp((size_t)CF * 128), bp(CF);
+      for (int n = 0; n < CF; ++n) {
+        for (int k = 0; k < 128; ++k) wp[(size_t)n * 128 + k] = W[(size_t)ref_ch(n) * 128 + k];
+        bp[n] = bb[ref_ch(n)];
+      }
+      asp2 = pack_conv(wp, CF, 128, 1, bp.data(), "");
+    }
+    {
+      const auto& W = P("bottleneck.weight");
+      const int K = 2 * CF;
+      std::vector<float> wp((size_t)embed_dim * K);
+      for (int n = 0; n < embed_dim; ++n)
+        for (int sidx = 0; sidx < 2; ++sidx)
+          for (int k = 0; k < CF; ++k)
+            wp[(size_t)n * K + sidx * CF + k] = W[(size_t)n * K + sidx * CF + ref_ch(k)];
+      simam_head = pack_lin(wp.data(), embed_dim, K, K, P("bottleneck.bias").data());
+    }
+  }
+
+  size_t simam_ws_floats(int B, int T, size_t* offs) const {
+    const int bc = resnet_chunk(B, T);
+    const RShapes r = resnet_shapes(T);
+    const size_t CF = (size_t)r.C4 * r.F4, cmax = (size_t)rblocks.back().out_planes;
+    const size_t nchunk = (size_t)std::max(1, ceil_div(2048, bc));
+    const size_t sizes[] = {bc * r.big, bc * r.big, bc * r.y1, bc * r.y2, bc * std::max<size_t>(r.sc, 1),
+                            (size_t)bc * 2 * CF,
+                            (size_t)bc * nchunk * 2 * cmax * 2,  // f64 moment partials
+                            (size_t)bc * 2 * cmax,                // mean / 1/(4(v+l))
+                            (size_t)bc * r.T4 * CF,               // frame rows [T][F*C]
+                            (size_t)bc * r.T4 * 128,              // attention hidden
+                            (size_t)bc * r.T4 * CF};              // attention logits
+    size_t o = 0;
+    for (int i = 0; i < 11; ++i) {
+      if (offs) offs[i] = o;
+      o += (sizes[i] + 63) / 64 * 64;
+    }
+    return o;
+  }
+
+  void forward_simam(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
+    const int bc = resnet_chunk(B, T);
+    size_t off[11];
+    simam_ws_floats(B, T, off);
+    float* X = ws + off[0];
+    float* O = ws + off[1];
+    float* Y1 = ws + off[2];
+    float* Z = ws + off[3];
+    float* SC = ws + off[4];
+    float* pooled = ws + off[5];
+    double* part = reinterpret_cast<double*>(ws + off[6]);
+    float* coef = ws + off[7];
+    float* Xt = ws + off[8];
+    float* att = ws + off[9];
+    float* logit = ws + off[10];
+    for (int b0 = 0; b0 < B; b0 += bc) {
+      const int nb = std::min(bc, B - b0);
+      int Fi = feat_dim, Ti = T, Ci = m_ch;
+      run("stem", 0, s, [&] {
+        launch_resnet_stem(feats + (size_t)b0 * T * feat_dim, nb, T, feat_dim, m_ch, stem_w, stem_b, X, s);
+      });
+      float* x = X;
+      float* o = O;
+      for (const RBlock& rb : rblocks) {
+        const int Fo = (Fi - 1) / rb.stride + 1, To = (Ti - 1) / rb.stride + 1;
+        const float* res = x;
+        if (rb.has_sc) {
+          gemm2d("shortcut", rb.sc, x, Ci, SC, rb.planes, nb, Fi, Ti, 1, rb.stride, 0, kActNone, nullptr, 0, s);
+          res = SC;
+        }
+        gemm2d("res_conv3x3", rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
+        gemm2d("res_conv3x3", rb.c2, Y1, rb.planes, Z, rb.planes, nb, Fo, To, 3, 1, 1, kActNone, nullptr, 0, s);
+        run("simam", 0, s, [&] { launch_simam(Z, res, o, nb, Fo * To, rb.planes, part, coef, s); });
+        std::swap(x, o);
+        Fi = Fo;
+        Ti = To;
+        Ci = rb.planes;
+      }
+      const int CF = Fi * Ci;
+      run("asp_rows", 0, s, [&] { launch_nhwc_to_tfc(x, Xt, nb, Fi, Ti, Ci, s); });
+      gemm("asp_linear1", asp1, Xt, CF, att, 128, nb * Ti, Ti, 1, 0, kActRelu, s);
+      gemm("asp_linear2", asp2, att, 128, logit, CF, nb * Ti, Ti, 1, 0, kActNone, s);
+      run("asp_pool_head", 0, s, [&] {
+        launch_astp_pool(logit, Xt, nb, Ti, CF, pooled, s, nullptr, 1e-5f);
+        launch_small_linear({pooled, 2 * CF, simam_head.wt, simam_head.bias, embed + (size_t)b0 * embed_dim,
+                             embed_dim, nb, 2 * CF, embed_dim, 0},
                             s);
       });
     }

@@ -250,7 +250,8 @@ void launch_residual_scale(const float* x, const float* h, const float* g, float
 namespace {
 __global__ __launch_bounds__(256) void astp_pool_kernel(const float* __restrict__ e,
                                                         const float* __restrict__ x, int T_, int C,
-                                                        float* __restrict__ out, const int* __restrict__ seg) {
+                                                        float* __restrict__ out, const int* __restrict__ seg,
+                                                        float floor_) {
   __shared__ float sm[4][4][64];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(256) void astp_pool_kernel(const float* __restrict_
     const float mean = A1 / S;
     const float var = A2 / S - mean * mean;
     out[(long)b * 2 * C + c] = mean;
-    out[(long)b * 2 * C + C + c] = sqrtf(fmaxf(var, 1e-7f));
+    out[(long)b * 2 * C + C + c] = sqrtf(fmaxf(var, floor_));
   }
 }
 
@@ -306,7 +307,8 @@ __global__ __launch_bounds__(256) void astp_pool_kernel(const float* __restrict_
 // per-lane branch).
 __global__ __launch_bounds__(256) void astp_pool4_kernel(const float* __restrict__ e,
                                                          const float* __restrict__ x, int T_, int C,
-                                                         float* __restrict__ out, const int* __restrict__ seg) {
+                                                         float* __restrict__ out, const int* __restrict__ seg,
+                                                         float floor_) {
   __shared__ f32x4 sm[4][4][64];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(256) void astp_pool4_kernel(const float* __restrict
         A2 += sm[w][3][lane][k] * f;
       }
       mean[k] = A1 / S;
-      sd[k] = sqrtf(fmaxf(A2 / S - mean[k] * mean[k], 1e-7f));
+      sd[k] = sqrtf(fmaxf(A2 / S - mean[k] * mean[k], floor_));
     }
     *reinterpret_cast<f32x4*>(out + (long)b * 2 * C + c) = mean;
     *reinterpret_cast<f32x4*>(out + (long)b * 2 * C + C + c) = sd;
@@ -367,16 +369,16 @@ __global__ __launch_bounds__(256) void astp_pool4_kernel(const float* __restrict
 }  // namespace
 
 void launch_astp_pool(const float* e, const float* x, int B, int T, int C, float* out,
-                      hipStream_t s, const int* seg) {
+                      hipStream_t s, const int* seg, float var_floor) {
   if (B == 0) return;
   const bool vec = C % 4 == 0 && ((reinterpret_cast<uintptr_t>(e) | reinterpret_cast<uintptr_t>(x) |
                                    reinterpret_cast<uintptr_t>(out)) & 15) == 0;
   if (vec) {
     dim3 grid(B, ceil_div(C, 256));
-    hipLaunchKernelGGL(astp_pool4_kernel, grid, dim3(256), 0, s, e, x, T, C, out, seg);
+    hipLaunchKernelGGL(astp_pool4_kernel, grid, dim3(256), 0, s, e, x, T, C, out, seg, var_floor);
   } else {
     dim3 grid(B, ceil_div(C, 64));
-    hipLaunchKernelGGL(astp_pool_kernel, grid, dim3(256), 0, s, e, x, T, C, out, seg);
+    hipLaunchKernelGGL(astp_pool_kernel, grid, dim3(256), 0, s, e, x, T, C, out, seg, var_floor);
   }
   WSP_HIP(hipGetLastError());
 }

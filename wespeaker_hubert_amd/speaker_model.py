@@ -113,13 +113,13 @@ class _HipHandle:
         arch, feat_dim, embed_dim, emb_bn, two_emb = self._create_args()
         _lib.check(lib.wsp_model_create(arch.encode(), feat_dim, embed_dim, int(emb_bn), int(two_emb),
                                         ctypes.byref(h)), "wsp_model_create")
-        n = lib.wsp_model_num_params(h)
         name = ctypes.c_char_p()
         ndim = ctypes.c_int()
         shape = (ctypes.c_int64 * 4)()
         try:
             for k in self._pre_finalize:
                 _lib.check(lib.wsp_model_set_option(h, k.encode(), self._options[k]), "set_option " + k)
+            n = lib.wsp_model_num_params(h)  # after the pre-finalize options (they may reshape the layout)
             for i in range(n):
                 _lib.check(lib.wsp_model_param_info(h, i, ctypes.byref(name), ctypes.byref(ndim), shape),
                            "param_info")
@@ -183,6 +183,9 @@ class HipSpeakerModel(_HipHandle):
         if self.spec.two_emb_layer:
             raise NotImplementedError("two_emb_layer=True is not implemented on the HIP path")
         self._layout = param_list(self.spec)
+        if self.spec.family == "simam" and self.spec.m_channels != 64:
+            self._options["in_planes"] = self.spec.m_channels  # before the weights (samresnet.py:124)
+            self._pre_finalize = ("in_planes",)
 
     def _create_args(self):
         s = self.spec
@@ -248,6 +251,10 @@ class HipSpeakerModel(_HipHandle):
         return self.spec.family == "ecapa"
 
     def __call__(self, feats: torch.Tensor):
+        # SimAM_ResNet*_ASP.forward returns the embedding itself (samresnet.py:135-143);
+        # ECAPA / ResNet return (aux, embed)
+        if self.spec.family == "simam":
+            return self.embed(feats)
         return None, self.embed(feats)
 
     forward = __call__
