@@ -62,6 +62,22 @@ def profiled_traffic(symbol: str, grid: int):
     return None, None
 
 
+def resnet_1x1_bytes_by_stage(arch: str, F: int, T: int, m: int = 32) -> dict:
+    """resnet_1x1_bytes_per_utt split by profiling sub-class (res_conv1x1.{c1,c3}.L<n>)."""
+    kind, nblocks = RESNET_ARCHS[arch]
+    out, cin, fi, ti = {}, m, F, T
+    for li, n in enumerate(nblocks):
+        p = m << li
+        for bi in range(n):
+            s = 2 if (li > 0 and bi == 0) else 1
+            fo, to = (fi - 1) // s + 1, (ti - 1) // s + 1
+            k1, k3 = f"res_conv1x1.c1.L{li + 1}", f"res_conv1x1.c3.L{li + 1}"
+            out[k1] = out.get(k1, 0.0) + 4.0 * fi * ti * (cin + p)
+            out[k3] = out.get(k3, 0.0) + 4.0 * fo * to * (p + 4 * p + 4 * p)
+            cin, fi, ti = 4 * p, fo, to
+    return out
+
+
 def resnet_1x1_bytes_per_utt(arch: str, F: int, T: int, m: int = 32) -> float:
     """Algorithmic HBM bytes of every 1x1 conv of one ResNet forward (resnet.py:72-107):
     fp32 activations read once (+ the residual read by conv3's epilogue), output written
@@ -249,6 +265,20 @@ def main():
         k = kernels.get("h_fc1") if hubert else kernels.get("conv1x1_CxC")
         kr = kernels.get("res_conv1x1") if args.arch.startswith("ResNet") else None
         k3 = kernels.get("res_conv3x3") if simam else None
+        if kr:
+            # per-stage HBM rate of the 1x1 convs (sub-classes of res_conv1x1)
+            for tag, bpu in resnet_1x1_bytes_by_stage(args.arch, 80, T).items():
+                n, ms, _ = model.profile_query(tag)
+                if n:
+                    kernels[tag] = {"launches_per_step": n // args.steps, "avg_ms": round(ms / n, 4),
+                                    "ms_per_step": round(ms / args.steps, 4),
+                                    "gbps": round(bpu * B / (ms / args.steps * 1e-3) / 1e9, 1)}
+            for li in range(1, 5):
+                n, ms, fl = model.profile_query(f"res_conv3x3.L{li}")
+                if n:
+                    kernels[f"res_conv3x3.L{li}"] = {"launches_per_step": n // args.steps, "avg_ms": round(ms / n, 4),
+                                                     "ms_per_step": round(ms / args.steps, 4),
+                                                     "tflops": round(fl / (ms / n * 1e-3) / 1e12, 2)}
         if k3:
             # MFMA roofline of the SimAM-ResNet 3x3 convs as a class (all launches of a step)
             ach = k3["tflops"] or 0.0
@@ -306,7 +336,8 @@ def main():
 
     gf = hubert_gflop_per_utt(N) + ecapa_gflop_per_utt(spec, T) if hubert else ecapa_gflop_per_utt(spec, T) \
         if args.arch.startswith("ECAPA") else simam_gflop_per_utt(spec, T) if simam else sum(
-        v["ms_per_step"] * (v["tflops"] or 0) for v in kernels.values()) / B if kernels else 0.0
+        v["ms_per_step"] * (v.get("tflops") or 0) for k, v in kernels.items() if "." not in k) / B \
+        if kernels else 0.0
     res = {
         "metric": "embeddings/sec on 5s 16kHz utts",
         "value": round(value, 2),

@@ -180,7 +180,14 @@ void Model::forward_segments(const float* feats, int B, const int* seg, int M, f
   m.forward_ecapa(feats, B, 1, embed, wsf, s, seg, M);  // T unused when segmented
 }
 
-void Model::profile(bool on) { impl->prof = on; }
+void Model::profile(bool on) {
+  if (on && !impl->prof)  // a new profiling window: drop the previous one's launches
+    for (auto& kv : impl->prof_map) {
+      kv.second.used = 0;
+      kv.second.flops = 0;
+    }
+  impl->prof = on;
+}
 
 void Model::set_option(const std::string& key, int value) {
   if (key == "precision") {
@@ -207,22 +214,27 @@ void Model::set_option(const std::string& key, int value) {
 }
 
 void Model::profile_query(const std::string& tag, int* launches, double* total_ms, double* flops) {
-  auto it = impl->prof_map.find(tag);
+  // `tag` names one kernel class or, as a prefix "tag.", every sub-class under it
+  // (e.g. "res_conv1x1" = "res_conv1x1.c1.L1" + ...).  Launches of the current /
+  // last profiling window.
   *launches = 0;
   *total_ms = 0;
   *flops = 0;
-  if (it == impl->prof_map.end()) return;
-  ProfEntry& e = it->second;
-  for (size_t i = 0; i < e.used; ++i) {
-    WSP_HIP(hipEventSynchronize(e.ev[i].second));
-    float ms = 0;
-    WSP_HIP(hipEventElapsedTime(&ms, e.ev[i].first, e.ev[i].second));
-    *total_ms += ms;
+  double fl = 0;
+  for (auto& kv : impl->prof_map) {
+    const std::string& k = kv.first;
+    if (k != tag && k.compare(0, tag.size() + 1, tag + ".") != 0) continue;
+    ProfEntry& e = kv.second;
+    for (size_t i = 0; i < e.used; ++i) {
+      WSP_HIP(hipEventSynchronize(e.ev[i].second));
+      float ms = 0;
+      WSP_HIP(hipEventElapsedTime(&ms, e.ev[i].first, e.ev[i].second));
+      *total_ms += ms;
+    }
+    *launches += (int)e.used;
+    fl += e.flops;
   }
-  *launches = (int)e.used;
-  *flops = e.used ? e.flops / (double)e.used : 0.0;
-  e.flops = 0;
-  e.used = 0;
+  *flops = *launches ? fl / (double)*launches : 0.0;
 }
 
 }  // namespace wsp

@@ -507,7 +507,17 @@ struct Model::Impl {
       });
       float* x = X;
       float* o = O;
+      // profiling sub-classes per stage: res_conv1x1.{c1,c3}.L<n>, res_conv3x3.L<n>
+      static const char* kC1[4] = {"res_conv1x1.c1.L1", "res_conv1x1.c1.L2", "res_conv1x1.c1.L3",
+                                   "res_conv1x1.c1.L4"};
+      static const char* kC3[4] = {"res_conv1x1.c3.L1", "res_conv1x1.c3.L2", "res_conv1x1.c3.L3",
+                                   "res_conv1x1.c3.L4"};
+      static const char* kK3[4] = {"res_conv3x3.L1", "res_conv3x3.L2", "res_conv3x3.L3", "res_conv3x3.L4"};
+      int ib = 0;
       for (const RBlock& rb : rblocks) {
+        int li = 0, acc = nblocks[0];
+        while (li < 3 && ib >= acc) acc += nblocks[++li];
+        ++ib;
         const int Fo = (Fi - 1) / rb.stride + 1, To = (Ti - 1) / rb.stride + 1;
         const float* res = x;
         if (rb.has_sc) {
@@ -515,12 +525,12 @@ struct Model::Impl {
           res = SC;
         }
         if (bottleneck) {
-          gemm1x1("res_conv1x1", rb.c1, x, Y1, nb * Fi * Ti, kActRelu, nullptr, s);
-          gemm2d("res_conv3x3", rb.c2, Y1, rb.planes, Y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
-          gemm1x1("res_conv1x1", rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
+          gemm1x1(kC1[li], rb.c1, x, Y1, nb * Fi * Ti, kActRelu, nullptr, s);
+          gemm2d(kK3[li], rb.c2, Y1, rb.planes, Y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
+          gemm1x1(kC3[li], rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
         } else {
-          gemm2d("res_conv3x3", rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
-          gemm2d("res_conv3x3", rb.c2, Y1, rb.planes, o, rb.out_planes, nb, Fo, To, 3, 1, 1, kActRelu, res,
+          gemm2d(kK3[li], rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
+          gemm2d(kK3[li], rb.c2, Y1, rb.planes, o, rb.out_planes, nb, Fo, To, 3, 1, 1, kActRelu, res,
                  rb.out_planes, s);
         }
         std::swap(x, o);
