@@ -295,14 +295,16 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
   const int r32 = lane & 31;
   const int h = lane >> 5;
   if (p.res) {
-    // one 32-row tile at a time: TN*16 residual loads in flight (register budget)
+    // every residual load of the wave's tiles issued before the first add: one
+    // HBM round trip per block instead of TM (the k-loop's staging registers are
+    // dead here, so TM*TN*16 values fit under the main loop's register peak)
     const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res);
     const int ldr4 = p.ldres * 4;
+    float rv[TM][TN][16];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row0 = m0 + (wm * TM + i) * 32 + 4 * h;
       const int lim = p.M - row0;
-      float rv[TN][16];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int base = row0 * ldr4 + (n0 + (wn * TN + j) * 32 + r32) * 4;
@@ -310,14 +312,16 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
         for (int r = 0; r < 16; ++r) {
           const int q = (r & 3) + 8 * (r >> 2);
           const int off = q < lim ? base + q * ldr4 : kOOB;
-          rv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, off, 0, 0));
+          rv[i][j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, off, 0, 0));
         }
       }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] += rv[j][r];
-    }
+        for (int r = 0; r < 16; ++r) acc[i][j][r] += rv[i][j][r];
   }
   if constexpr (WM > 0) {
     if (p.colsum) {  // fused per-utterance column sums (host: uniform batch, T >= BM, no row bias)
