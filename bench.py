@@ -78,6 +78,35 @@ def resnet_1x1_bytes_by_stage(arch: str, F: int, T: int, m: int = 32) -> dict:
     return out
 
 
+def resnet_1x1_launch_geometry(arch: str, F: int, T: int, bc: int, m: int = 32) -> dict:
+    """Per 1x1 sub-class: (kernel symbol, grid threads) of its launches at `bc`
+    utterances per launch — the tile launch_conv_gemm_x3 picks for N at the ResNet
+    default variant 3 (N % 64: 128x32, N % 128: 128x64, else 128x128 swizzled)."""
+    kind, nblocks = RESNET_ARCHS[arch]
+    out, fi, ti = {}, F, T
+
+    def launch(rows, N):
+        if N % 64:
+            tmpl, swz, bn = "4ELi1ELi1ELi1", 0, 32
+        elif N % 128:
+            tmpl, swz, bn = "4ELi1ELi1ELi2", 0, 64
+        else:
+            tmpl, swz, bn = "2ELi2ELi2ELi2", 1, 128
+        sym = f"_ZN3wsp12_GLOBAL__N_112conv_gemm_x3ILi{tmpl}ELi0ELb1ELi0ELb0ELb{swz}E"
+        return sym, ((bc * rows + 127) // 128) * (N // bn) * 256
+
+    for li, n in enumerate(nblocks):
+        p = m << li
+        s = 2 if li > 0 else 1
+        fo, to = (fi - 1) // s + 1, (ti - 1) // s + 1
+        # (symbol, grid, launches per chunk); a stride-2 first block's conv1 runs at the input resolution
+        c1 = [(*launch(fi * ti, p), 1), (*launch(fo * to, p), n - 1)] if s == 2 else [(*launch(fo * to, p), n)]
+        out[f"res_conv1x1.c1.L{li + 1}"] = [x for x in c1 if x[2] > 0]
+        out[f"res_conv1x1.c3.L{li + 1}"] = [(*launch(fo * to, 4 * p), n)]
+        fi, ti = fo, to
+    return out
+
+
 def resnet_1x1_bytes_per_utt(arch: str, F: int, T: int, m: int = 32) -> float:
     """Algorithmic HBM bytes of every 1x1 conv of one ResNet forward (resnet.py:72-107):
     fp32 activations read once (+ the residual read by conv3's epilogue), output written
@@ -265,14 +294,28 @@ def main():
         k = kernels.get("h_fc1") if hubert else kernels.get("conv1x1_CxC")
         kr = kernels.get("res_conv1x1") if args.arch.startswith("ResNet") else None
         k3 = kernels.get("res_conv3x3") if simam else None
+        traffic_step, traffic_srcs = 0.0, set()
         if kr:
-            # per-stage HBM rate of the 1x1 convs (sub-classes of res_conv1x1)
+            # per-stage HBM rate of the 1x1 convs (sub-classes of res_conv1x1), and the
+            # class's PMC traffic per step: profiled bytes per launch of each sub-class's
+            # (symbol, grid) x its launches per step
+            bc = B // -(-B // 64) if B > 64 else B  # the model's 2-GiB chunking at T = 498
+            geo = resnet_1x1_launch_geometry(args.arch, 80, T, bc)
             for tag, bpu in resnet_1x1_bytes_by_stage(args.arch, 80, T).items():
                 n, ms, _ = model.profile_query(tag)
                 if n:
                     kernels[tag] = {"launches_per_step": n // args.steps, "avg_ms": round(ms / n, 4),
                                     "ms_per_step": round(ms / args.steps, 4),
                                     "gbps": round(bpu * B / (ms / args.steps * 1e-3) / 1e9, 1)}
+                    if traffic_step is not None and tag in geo:
+                        chunks = (n // args.steps) // sum(c for _, _, c in geo[tag])
+                        for sym, grid, cnt in geo[tag]:
+                            tb, src = profiled_traffic(sym, grid)
+                            if tb is None:
+                                traffic_step = None
+                                break
+                            traffic_step += tb * cnt * chunks
+                            traffic_srcs.add(src.split(":")[0])
             for li in range(1, 5):
                 n, ms, fl = model.profile_query(f"res_conv3x3.L{li}")
                 if n:
@@ -295,7 +338,9 @@ def main():
             ach = byts / (kr["ms_per_step"] * 1e-3) / 1e9
             roof = {"kernel": "conv_gemm_x3 ResNet 1x1 convs (res_conv1x1, all launches of a step)",
                     "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None, "traffic_source": None,
+                    "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic_step or None,
+                    "traffic_source": ",".join(sorted(traffic_srcs)) or None,
+                    "traffic_note": "PMC HBM bytes of all 1x1 launches of a step (FETCH_SIZE x2 + WRITE_SIZE)",
                     "algorithmic_bytes": byts, "launches_per_step": kr["launches_per_step"],
                     "ms_per_step": kr["ms_per_step"]}
         elif k and hubert:
