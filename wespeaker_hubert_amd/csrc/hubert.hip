@@ -80,42 +80,50 @@ __global__ __launch_bounds__(kC0) void conv0_kernel(const float* __restrict__ wa
 }
 
 // ------------------------------------------------------------ layernorm ---
-template <int VPL>
+// One wave per row, 16-B accesses: lane owns channels 4*lane + 256*i (i < V4).
+// The remapped residual (pos_conv's 64-wide group padding) keeps 4-aligned
+// channel runs inside one group (gin % 4 == 0), so it is read as float4 too.
+template <int V4>
 __global__ __launch_bounds__(256) void layernorm_kernel(const LayerNormArgs p) {
-  constexpr int D = VPL * 64;
+  constexpr int D = V4 * 256;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= p.M) return;
-  float v[VPL];
+  f32x4 v[V4];
   const float* x = p.x + (size_t)row * p.ldx;
 #pragma unroll
-  for (int i = 0; i < VPL; ++i) v[i] = x[lane + 64 * i];
+  for (int i = 0; i < V4; ++i) v[i] = *reinterpret_cast<const f32x4*>(x + 4 * lane + 256 * i);
   if (p.add) {
     const float* a = p.add + (size_t)row * p.ldadd;
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int c = lane + 64 * i;
+    for (int i = 0; i < V4; ++i) {
+      const int c = 4 * lane + 256 * i;
       const int g = c / p.gin;
-      v[i] += a[g * p.gout + (c - g * p.gin)];
+      v[i] += *reinterpret_cast<const f32x4*>(a + g * p.gout + (c - g * p.gin));
     }
   }
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < VPL; ++i) s += v[i];
+  for (int i = 0; i < V4; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
   const float mean = wave_sum(s) * (1.f / D);
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < VPL; ++i) {
-    v[i] -= mean;
-    q = fmaf(v[i], v[i], q);
-  }
+  for (int i = 0; i < V4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[i][e] -= mean;
+      q = fmaf(v[i][e], v[i][e], q);
+    }
   const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / D) + p.eps);
   float* o = p.out + (size_t)row * p.ldo;
 #pragma unroll
-  for (int i = 0; i < VPL; ++i) {
-    const int c = lane + 64 * i;
-    v[i] = v[i] * rstd * p.gamma[c] + p.beta[c];
-    o[c] = v[i];
+  for (int i = 0; i < V4; ++i) {
+    const int c = 4 * lane + 256 * i;
+    const f32x4 g = *reinterpret_cast<const f32x4*>(p.gamma + c);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(p.beta + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[i][e] = v[i][e] * rstd * g[e] + b[e];
+    *reinterpret_cast<f32x4*>(o + c) = v[i];
   }
   if (p.feat) {
     // s3prl Featurizer: feat += w_l * h_l; length match replicates the last
@@ -139,9 +147,16 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LayerNormArgs p) {
     for (int tt = t; tt < t_end; ++tt) {
       float* f = p.feat + (fbase + tt) * D;
 #pragma unroll
-      for (int i = 0; i < VPL; ++i) {
-        const int c = lane + 64 * i;
-        f[c] = p.feat_init ? p.feat_w * v[i] : fmaf(p.feat_w, v[i], f[c]);
+      for (int i = 0; i < V4; ++i) {
+        f32x4* fp = reinterpret_cast<f32x4*>(f + 4 * lane + 256 * i);
+        if (p.feat_init) {
+          *fp = p.feat_w * v[i];
+        } else {
+          f32x4 acc = *fp;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] = fmaf(p.feat_w, v[i][e], acc[e]);
+          *fp = acc;
+        }
       }
     }
   }
@@ -359,14 +374,16 @@ void launch_hubert_conv0(const float* wav, int B, int N, int ldw, int T0, const 
 
 void launch_layernorm(const LayerNormArgs& p, hipStream_t s) {
   WSP_CHECK(p.M > 0 && (p.D == 512 || p.D == 768), "layernorm: D must be 512 or 768");
-  WSP_CHECK(!p.add || (p.gin > 0 && p.gout >= p.gin), "layernorm: bad add remap");
+  WSP_CHECK(!p.add || (p.gin > 0 && p.gout >= p.gin && p.gin % 4 == 0 && p.gout % 4 == 0 && p.ldadd % 4 == 0),
+            "layernorm: bad add remap");
+  WSP_CHECK(p.ldx % 4 == 0 && p.ldo % 4 == 0, "layernorm: rows must be 16-B aligned");
   WSP_CHECK(!p.feat || p.seg || (p.T > 0 && p.Tout > 0 && p.M % p.T == 0), "layernorm: bad featurizer shape");
   WSP_CHECK(!p.seg || (p.fseg && p.nseg > 0), "layernorm: segmented featurizer needs output offsets");
   const dim3 grid((p.M + 3) / 4);
   if (p.D == 512)
-    hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, s, p);
+    hipLaunchKernelGGL(layernorm_kernel<2>, grid, dim3(256), 0, s, p);
   else
-    hipLaunchKernelGGL(layernorm_kernel<12>, grid, dim3(256), 0, s, p);
+    hipLaunchKernelGGL(layernorm_kernel<3>, grid, dim3(256), 0, s, p);
   WSP_HIP(hipGetLastError());
 }
 

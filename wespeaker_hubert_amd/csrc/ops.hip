@@ -7,20 +7,22 @@ namespace wsp {
 
 // ----------------------------------------------------------- small linear ---
 // out[r][n] = act(bias[n] + sum_k in[r][k] * wt[k][n]) for the row-batched
-// GEMVs (SE FCs, GLOB context bias, BN-folded embedding head): R = batch rows,
-// K <= a few thousand.  One workgroup = kRB rows x 64 outputs (lane = output,
-// coalesced k-major weight reads); the 4 waves split K and reduce through LDS.
-// Input rows are wave-uniform (scalar loads).
+// GEMVs (SE FCs, GLOB context bias, BN-folded embedding heads): R = batch rows,
+// K up to ~20k (ResNet293's 20480-wide TSTP statistics).  One workgroup = kRB
+// rows x 64 outputs (lane = output, coalesced k-major weight reads); its kSW
+// waves split K (short per-wave dependency chains: latency, not bandwidth, bounds
+// these) and reduce through LDS in a fixed order.  Input rows are wave-uniform.
 namespace {
 constexpr int kRB = 4;
+constexpr int kSW = 16;
 
-__global__ __launch_bounds__(256) void small_linear_kernel(const SmallLinearArgs p) {
-  __shared__ float part[4][kRB][64];
+__global__ __launch_bounds__(64 * kSW) void small_linear_kernel(const SmallLinearArgs p) {
+  __shared__ float part[kSW][kRB][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int n = blockIdx.y * 64 + lane;
   const int r0 = blockIdx.x * kRB;
-  const int kq = (p.K + 3) / 4;
+  const int kq = (p.K + kSW - 1) / kSW;
   const int k0 = wave * kq, k1 = min(p.K, k0 + kq);
   float acc[kRB];
 #pragma unroll
@@ -53,17 +55,17 @@ __global__ __launch_bounds__(256) void small_linear_kernel(const SmallLinearArgs
 #pragma unroll
   for (int r = 0; r < kRB; ++r) part[wave][r][lane] = acc[r];
   __syncthreads();
-  if (wave == 0 && n < p.N) {
-    const float bv = p.bias ? p.bias[n] : 0.f;
+  if (wave < kRB && n < p.N) {  // wave r finishes row r
+    const int r = wave;
+    if (r0 + r >= p.R) return;
+    float y = 0.f;
 #pragma unroll
-    for (int r = 0; r < kRB; ++r) {
-      if (r0 + r >= p.R) break;
-      float y = ((part[0][r][lane] + part[1][r][lane]) + (part[2][r][lane] + part[3][r][lane])) + bv;
-      if (p.act == 1) y = fmaxf(y, 0.f);
-      else if (p.act == 2) y = tanhf(y);
-      else if (p.act == 3) y = 1.f / (1.f + expf(-y));
-      p.out[(long)(r0 + r) * p.ldo + n] = y;
-    }
+    for (int w = 0; w < kSW; ++w) y += part[w][r][lane];
+    y += p.bias ? p.bias[n] : 0.f;
+    if (p.act == 1) y = fmaxf(y, 0.f);
+    else if (p.act == 2) y = tanhf(y);
+    else if (p.act == 3) y = 1.f / (1.f + expf(-y));
+    p.out[(long)(r0 + r) * p.ldo + n] = y;
   }
 }
 }  // namespace
@@ -71,7 +73,7 @@ __global__ __launch_bounds__(256) void small_linear_kernel(const SmallLinearArgs
 void launch_small_linear(const SmallLinearArgs& p, hipStream_t s) {
   if (p.R == 0) return;
   dim3 grid(ceil_div(p.R, kRB), ceil_div(p.N, 64));
-  hipLaunchKernelGGL(small_linear_kernel, grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL(small_linear_kernel, grid, dim3(64 * kSW), 0, s, p);
   WSP_HIP(hipGetLastError());
 }
 
