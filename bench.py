@@ -32,14 +32,24 @@ from wespeaker_hubert_amd.synthetic import synth_audio, synth_state_dict  # noqa
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (no sparsity)
 HBM_PEAK_GBPS = 8000.0
-DOMINANT = {  # kernel-symbol prefix of the SE-Res2Block 1x1 CxC conv (ConvGemmArgs.role == 1)
-    1: "_ZN3wsp12_GLOBAL__N_112conv_gemm_x3ILi4ELi2ELi2ELi2ELi0ELb1ELi1E",
-    0: "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1E",
-}
-DOMINANT_GEMM = {  # plain (role 0) 1-D GEMM: the HuBERT FFN fc1 (M = B*T, N = 3072, K = 768)
-    1: "_ZN3wsp12_GLOBAL__N_112conv_gemm_x3ILi4ELi2ELi2ELi2ELi0ELb1ELi0ELb0E",
-    0: "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1E",
-}
+def x3_tile(variant, N: int, K: int):
+    """(template prefix, BM, BN, threads) of the bf16x3 block launch_conv_gemm_x3 picks."""
+    v = 5 if variant is None else variant
+    if v == 5 and N % 256 == 0 and K >= 2048:
+        return "ILi4ELi2ELi2ELi4E", 256, 256, 512
+    if v in (1, 4, 5):
+        return "ILi4ELi2ELi2ELi2E", 256, 128, 512
+    return "ILi2ELi2ELi2ELi2E", 128, 128, 256
+
+
+def dominant_symbol(precision: int, variant, N: int, K: int, role: int):
+    """Kernel-symbol prefix and block geometry of the SE-Res2Block 1x1 CxC conv
+    (role 1) or a plain role-0 1-D GEMM (the HuBERT FFN fc1)."""
+    if precision == 0:
+        return "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1E", 128, 128, 256
+    t, bm, bn, nt = x3_tile(variant, N, K)
+    sym = f"_ZN3wsp12_GLOBAL__N_112conv_gemm_x3{t}Li0ELb1ELi{role}E" + ("" if role else "Lb0E")
+    return sym, bm, bn, nt
 HUBERT_ARCH = "HuBERT_ECAPA_GLOB_c512"  # C4: HuBERT-base front end + ECAPA_TDNN_GLOB_c512(feat_dim 768)
 HEAD_TAGS = ("layer1", "conv1x1_CxC", "res2_k3", "se", "conv_cat", "glob_ctx", "pool_linear1", "pool_linear2",
              "astp", "head", "stem", "shortcut", "res_conv1x1", "res_conv3x3", "tstp_head",
@@ -350,8 +360,8 @@ def main():
             ach = flops / (k["avg_ms"] * 1e-3) / 1e12
             x3 = args.precision == 1
             peak = BF16_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
-            sym = DOMINANT_GEMM[args.precision]
-            grid = ((M + 255) // 256) * (Nn // 128) * 512 if x3 else ((M + 127) // 128) * (Nn // 128) * 256
+            sym, bm, bn, nt = dominant_symbol(args.precision, args.x3_variant, Nn, K, 0)
+            grid = ((M + bm - 1) // bm) * (Nn // bn) * nt
             traffic, src = profiled_traffic(sym, grid)
             roof = {"kernel": sym + " (HuBERT FFN fc1 + GELU)", "bound": "mfma", "achieved": round(ach, 2),
                     "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
@@ -367,8 +377,8 @@ def main():
             ach = flops / (k["avg_ms"] * 1e-3) / 1e12
             x3 = args.precision == 1
             peak = BF16_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
-            sym = DOMINANT[args.precision]
-            grid = (M // 256) * (C // 128) * 512 if x3 else ((M + 127) // 128) * (C // 128) * 256
+            sym, bm, bn, nt = dominant_symbol(args.precision, args.x3_variant, C, C, 1)
+            grid = ((M + bm - 1) // bm) * (C // bn) * nt
             traffic, src = profiled_traffic(sym, grid)
             algo_bytes = 4.0 * M * C * 2 + (2 if x3 else 4) * C * C * (2 if x3 else 1)
             roof = {"kernel": sym, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,

@@ -95,7 +95,7 @@ int main(int argc, char** argv) {
     struct V {
       const char* name;
       int kind;
-    } vars[] = {{"x3_256x128", 1}, {"x3_128x128", 0}, {"x3_dma", 2}, {"x3_128swz", 3}, {"x3_256swz", 4}, {"f32", -1}};
+    } vars[] = {{"x3_256x128", 1}, {"x3_128x128", 0}, {"x3_dma", 2}, {"x3_128swz", 3}, {"x3_256swz", 4}, {"x3_256sq", 5}, {"f32", -1}};
     std::vector<float> ref((size_t)M * N), out((size_t)M * N);
     for (auto& v : vars) {
       ConvGemmArgs q = g;

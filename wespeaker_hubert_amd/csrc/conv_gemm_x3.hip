@@ -11,7 +11,10 @@
 // pooling_layers.py:105-117).
 //
 // Tiling: NW waves (4 or 8), block BM x BN x BK=32, each wave TM x TN tiles
-// of 32x32 (v_mfma_f32_32x32x16_bf16).  A (fp32 activations) is split into
+// of 32x32 (v_mfma_f32_32x32x16_bf16).  The default (variant 5) adds, for deep
+// contractions (K >= 2048), a 256 x 256 block of 8 waves with 64 x 128 per wave
+// (12 fragment reads per 24 MFMAs instead of 8 per 12) and ONE register staging
+// set — its 128 accumulators leave no room for a second.  A (fp32 activations) is split into
 // hi/lo bf16 while staging; W is pre-split on the host.  LDS rows are
 // 32 bf16 + 8 pad (80 B): the 16-byte fragment reads (row = lane&31,
 // k = 16 s + 8 (lane>>5)) hit 16 distinct slots per ds_read_b128 group.
@@ -42,7 +45,8 @@ struct Lds {
   }
 };
 
-template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D = false, bool SWZ = false>
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D = false, bool SWZ = false,
+          int NSET = 2>
 __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArgs p,
                                                                const __bf16* __restrict__ whi,
                                                                const __bf16* __restrict__ wlo) {
@@ -100,7 +104,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   // Two register sets: tile k+1 is converted and written to LDS while tile k
   // is multiplied, and tile k+2 is in flight (loads get a whole k-step of
   // MFMA time to land before anyone waits on them).
-  f32x4 ra0[AR], ra1[AR];
+  f32x4 ra0[AR], ra1[AR];  // (ra1 / rb1 unused with NSET == 1)
   bf16x8 rb0[BR], rb1[BR];
 
   auto load_tile = [&](f32x4 (&ra)[AR], bf16x8 (&rb)[BR], int k0, bool live) {
@@ -173,6 +177,25 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   };
 
   const int nk = p.Kp / BK;
+  if constexpr (NSET == 1) {
+    // One register set (wide wave tiles: the accumulators leave no room for a
+    // second): tile k+1, loaded during step k-1, is written to the free buffer
+    // between step k's two sub-steps, and tile k+2 is issued right after it.
+    load_tile(ra0, rb0, 0, true);
+    store_tile(ra0, rb0, 0);
+    load_tile(ra0, rb0, BK, true);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      mma_step(buf, 0);
+      store_tile(ra0, rb0, buf ^ 1);  // past-the-end tiles are zeros nobody reads
+      load_tile(ra0, rb0, (kt + 2) * BK, kt + 2 < nk);
+      mma_step(buf, 1);
+      __syncthreads();
+    }
+    gemm_epilogue<TM, TN, WM, WN>(p, acc, m0, n0, wm, wn, lane, smem);
+    return;
+  }
   load_tile(ra0, rb0, 0, true);
   load_tile(ra1, rb1, BK, true);
   store_tile(ra0, rb0, 0);
@@ -200,35 +223,35 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   gemm_epilogue<TM, TN, WM, WN>(p, acc, m0, n0, wm, wn, lane, smem);
 }
 
-template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D, bool SWZ>
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D, bool SWZ, int NSET>
 void launch_x3_k(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
   constexpr int ROWB = Lds<SWZ>::ROWB;
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const size_t lds = (size_t)2 * (2 * BM * ROWB + 2 * BN * ROWB + Lds<SWZ>::SKEW);
-  hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, AMODE, UNI, ROLE, C2D, SWZ>), dim3(nwg), dim3(NT), lds, s,
+  hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, AMODE, UNI, ROLE, C2D, SWZ, NSET>), dim3(nwg), dim3(NT), lds, s,
                      p, whi, wlo);
   WSP_HIP(hipGetLastError());
 }
 
-template <int WM, int WN, int TM, int TN, bool SWZ = false>
+template <int WM, int WN, int TM, int TN, bool SWZ = false, int NSET = 2>
 void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
   if (p.conv2d) {
-    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, true, SWZ>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, true, SWZ, NSET>(p, whi, wlo, s);
     return;
   }
   const bool uni = uniform_ktiles(p);
   if (p.amode == kAAdd) {
     if (uni)
-      launch_x3_k<WM, WN, TM, TN, kAAdd, true, 0, false, SWZ>(p, whi, wlo, s);
+      launch_x3_k<WM, WN, TM, TN, kAAdd, true, 0, false, SWZ, NSET>(p, whi, wlo, s);
     else
-      launch_x3_k<WM, WN, TM, TN, kAAdd, false, 0, false, SWZ>(p, whi, wlo, s);
+      launch_x3_k<WM, WN, TM, TN, kAAdd, false, 0, false, SWZ, NSET>(p, whi, wlo, s);
   } else if (!uni) {
-    launch_x3_k<WM, WN, TM, TN, kACat, false, 0, false, SWZ>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, false, 0, false, SWZ, NSET>(p, whi, wlo, s);
   } else if (p.role == 1) {
-    launch_x3_k<WM, WN, TM, TN, kACat, true, 1, false, SWZ>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 1, false, SWZ, NSET>(p, whi, wlo, s);
   } else {
-    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, false, SWZ>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, false, SWZ, NSET>(p, whi, wlo, s);
   }
 }
 
@@ -237,7 +260,7 @@ void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo,
 int conv_gemm_x3_block_rows(const ConvGemmArgs& p, int variant) {
   if (p.N % 64 != 0 || (p.gcols && p.gcols % 64 != 0)) return 128;
   if (p.gcols || p.N % 128 != 0) return 128;
-  return (variant == 1 || variant == 4) ? 256 : 128;
+  return (variant == 1 || variant == 4 || variant == 5) ? 256 : 128;
 }
 
 namespace {
@@ -271,7 +294,7 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
   if (p.colsum) {
     const int bm = conv_gemm_x3_block_rows(p, variant);
     WSP_CHECK(!p.seg && !p.row_bias && !p.conv2d && p.T >= bm && (variant == 1 || variant == 3 || variant == 4 ||
-                                                                  variant == 0),
+                                                                  variant == 5 || variant == 0),
               "conv_gemm_x3: column sums need a uniform batch with T >= block rows and no row bias");
   }
   WSP_CHECK(p.Kp % 64 == 0, "conv_gemm_x3: packed K must be a multiple of 64");
@@ -289,6 +312,14 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
     launch_x3_tile<2, 2, 2, 2, true>(p, h, l, s);  // 128 x 128, 4 waves, swizzled rows: 2 blocks / CU
   } else if (variant == 4) {
     launch_x3_tile<4, 2, 2, 2, true>(p, h, l, s);  // 256 x 128, 8 waves, swizzled rows
+  } else if (variant == 5) {
+    // 256 x 256 only for deep contractions: in-model it wins at K = 3072 (ECAPA conv_cat
+    // -7 %, HuBERT fc2 -13 %) and loses at K <= 1536 (fc1 +19 %, C x C +5 %): its
+    // fewer, longer blocks pay a bigger per-block prologue / epilogue and grid tail
+    if (p.N % 256 == 0 && !p.gcols && p.Kp >= 2048)
+      launch_x3_tile<4, 2, 2, 4, true, 1>(p, h, l, s);  // 256 x 256, 8 waves (4 x 2), 64 x 128 per wave
+    else
+      launch_x3_tile<4, 2, 2, 2, true>(p, h, l, s);  // variant 4
   } else {
     launch_x3_tile<2, 2, 2, 2>(p, h, l, s);  // 128 x 128, 4 waves
   }

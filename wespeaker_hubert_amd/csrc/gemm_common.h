@@ -298,30 +298,35 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
     // every residual load of the wave's tiles issued before the first add: one
     // HBM round trip per block instead of TM (the k-loop's staging registers are
     // dead here, so TM*TN*16 values fit under the main loop's register peak)
+    // (waves with more than 4 tiles: 4 tiles' worth at a time)
     const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res);
     const int ldr4 = p.ldres * 4;
-    float rv[TM][TN][16];
+    constexpr int TMG = (TM * TN <= 4) ? TM : (4 / TN > 0 ? 4 / TN : 1);  // tile rows per group
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row0 = m0 + (wm * TM + i) * 32 + 4 * h;
-      const int lim = p.M - row0;
+    for (int i0 = 0; i0 < TM; i0 += TMG) {
+      float rv[TMG][TN][16];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int base = row0 * ldr4 + (n0 + (wn * TN + j) * 32 + r32) * 4;
+      for (int ii = 0; ii < TMG; ++ii) {
+        const int row0 = m0 + (wm * TM + i0 + ii) * 32 + 4 * h;
+        const int lim = p.M - row0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int q = (r & 3) + 8 * (r >> 2);
-          const int off = q < lim ? base + q * ldr4 : kOOB;
-          rv[i][j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, off, 0, 0));
+        for (int j = 0; j < TN; ++j) {
+          const int base = row0 * ldr4 + (n0 + (wn * TN + j) * 32 + r32) * 4;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int q = (r & 3) + 8 * (r >> 2);
+            const int off = q < lim ? base + q * ldr4 : kOOB;
+            rv[ii][j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, off, 0, 0));
+          }
         }
       }
+#pragma unroll
+      for (int ii = 0; ii < TMG; ++ii)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i0 + ii][j][r] += rv[ii][j][r];
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] += rv[i][j][r];
   }
   if constexpr (WM > 0) {
     if (p.colsum) {  // fused per-utterance column sums (host: uniform batch, T >= BM, no row bias)

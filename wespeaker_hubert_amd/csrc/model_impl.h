@@ -188,7 +188,7 @@ struct Model::Impl {
 
   // 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA
   int precision = 1;
-  int x3_variant = 4;  // 256 x 128 swizzled-LDS bf16x3 tiles (tools/gemm_bench: +3-8 % over 1)
+  int x3_variant = 5;  // 256 x 256 bf16x3 tiles where N % 256 == 0, else 256 x 128 (tools/gemm_bench)
 
   // profiling
   bool prof = false;
@@ -474,7 +474,7 @@ struct Model::Impl {
     g.kw = kw;
     g.res = res;
     g.ldres = ldres;
-    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 4 : x3_variant, s); });
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 5 : x3_variant, s); });
   }
   void gemm1x1(const char* tag, const ConvW& cw, const float* a0, float* out, int M, int act, const float* res,
                hipStream_t s) {
@@ -486,7 +486,7 @@ struct Model::Impl {
     fill(g, cw, M, M, 1, 0, out, cw.N, act, nullptr, true);
     g.res = res;
     g.ldres = cw.N;
-    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 4 : x3_variant, s); });
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 5 : x3_variant, s); });
   }
 
   void forward_resnet(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
@@ -808,7 +808,7 @@ struct Model::Impl {
     if (precision == 1 && x3_variant == 2 && conv_gemm_dma_supported(g))
       launch_conv_gemm_dma(g, cw.whi, cw.wlo, s);
     else if (precision == 1)
-      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 4 : x3_variant, s);
+      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 5 : x3_variant, s);
     else
       launch_conv_gemm(g, s);
   }
@@ -876,7 +876,7 @@ struct Model::Impl {
     double* sesum = reinterpret_cast<double*>(ws + off[16]);
     // SE squeeze fused into conv3's epilogue (per-utterance f64 column sums) on the
     // bf16x3 path for uniform batches whose utterances span >= one block of rows
-    const int se_bm = precision == 1 ? conv_gemm_x3_block_rows(ConvGemmArgs{.N = C}, x3_variant == 2 ? 4 : x3_variant) : 0;
+    const int se_bm = precision == 1 ? conv_gemm_x3_block_rows(ConvGemmArgs{.N = C}, x3_variant == 2 ? 5 : x3_variant) : 0;
     const bool se_fused = precision == 1 && !seg && T >= se_bm;
 
     gemm("layer1", layer1, feats, feat_dim, x[1], C, M, T, 1, 2, kActRelu, s);
