@@ -32,12 +32,12 @@ from wespeaker_hubert_amd.synthetic import synth_audio, synth_state_dict  # noqa
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (no sparsity)
 HBM_PEAK_GBPS = 8000.0
-def x3_tile(variant, N: int, K: int):
+def x3_tile(variant, N: int, K: int, gelu: bool = False):
     """(template prefix, BM, BN, threads) of the bf16x3 block launch_conv_gemm_x3 picks."""
     v = 5 if variant is None else variant
-    if v == 5 and N % 256 == 0 and K >= 2048:
+    if (v == 6 or (v == 5 and (not gelu or K >= 2048))) and N % 256 == 0:
         return "ILi4ELi2ELi2ELi4E", 256, 256, 512
-    if v in (1, 4, 5):
+    if v in (1, 4, 5, 6):
         return "ILi4ELi2ELi2ELi2E", 256, 128, 512
     return "ILi2ELi2ELi2ELi2E", 128, 128, 256
 
@@ -47,7 +47,7 @@ def dominant_symbol(precision: int, variant, N: int, K: int, role: int):
     (role 1) or a plain role-0 1-D GEMM (the HuBERT FFN fc1)."""
     if precision == 0:
         return "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1E", 128, 128, 256
-    t, bm, bn, nt = x3_tile(variant, N, K)
+    t, bm, bn, nt = x3_tile(variant, N, K, gelu=(role == 0))  # role 0 here = HuBERT fc1 (GELU)
     sym = f"_ZN3wsp12_GLOBAL__N_112conv_gemm_x3{t}Li0ELb1ELi{role}E" + ("" if role else "Lb0E")
     return sym, bm, bn, nt
 HUBERT_ARCH = "HuBERT_ECAPA_GLOB_c512"  # C4: HuBERT-base front end + ECAPA_TDNN_GLOB_c512(feat_dim 768)

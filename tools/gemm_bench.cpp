@@ -47,7 +47,8 @@ int main(int argc, char** argv) {
     std::mt19937 rng(1);
     std::uniform_real_distribution<float> ua(-1.f, 1.f), uw(-0.05f, 0.05f);
     std::vector<float> a((size_t)M * cin), w((size_t)N * Kp, 0.f), bias(N);
-    for (auto& x : a) x = ua(rng);
+    const bool relu_a = std::getenv("GB_RELU_A") != nullptr;  // post-ReLU activations: half zeros
+    for (auto& x : a) x = relu_a ? std::fmax(ua(rng), 0.f) : ua(rng);
     for (int n = 0; n < N; ++n)
       for (int k = 0; k < K; ++k) w[(size_t)n * Kp + k] = uw(rng);
     for (auto& x : bias) x = uw(rng);
@@ -86,7 +87,7 @@ int main(int argc, char** argv) {
     g.Kp = Kp;
     g.bias = db;
     g.ldo = N;
-    g.act = kActRelu;
+    g.act = std::getenv("GB_ACT") ? std::atoi(std::getenv("GB_ACT")) : kActRelu;
     hipStream_t s;
     CK(hipStreamCreate(&s));
     hipEvent_t e0, e1;
@@ -95,7 +96,7 @@ int main(int argc, char** argv) {
     struct V {
       const char* name;
       int kind;
-    } vars[] = {{"x3_256x128", 1}, {"x3_128x128", 0}, {"x3_dma", 2}, {"x3_128swz", 3}, {"x3_256swz", 4}, {"x3_256sq", 5}, {"f32", -1}};
+    } vars[] = {{"x3_256x128", 1}, {"x3_128x128", 0}, {"x3_dma", 2}, {"x3_128swz", 3}, {"x3_256swz", 4}, {"x3_256sq", 5}, {"x3_256sq_any", 6}, {"f32", -1}};
     std::vector<float> ref((size_t)M * N), out((size_t)M * N);
     for (auto& v : vars) {
       ConvGemmArgs q = g;

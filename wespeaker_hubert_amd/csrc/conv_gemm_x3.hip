@@ -11,10 +11,10 @@
 // pooling_layers.py:105-117).
 //
 // Tiling: NW waves (4 or 8), block BM x BN x BK=32, each wave TM x TN tiles
-// of 32x32 (v_mfma_f32_32x32x16_bf16).  The default (variant 5) adds, for deep
-// contractions (K >= 2048), a 256 x 256 block of 8 waves with 64 x 128 per wave
-// (12 fragment reads per 24 MFMAs instead of 8 per 12) and ONE register staging
-// set — its 128 accumulators leave no room for a second.  A (fp32 activations) is split into
+// of 32x32 (v_mfma_f32_32x32x16_bf16).  The default (variant 5) uses, where
+// N % 256 == 0, a 256 x 256 block of 8 waves with 64 x 128 per wave (12 fragment
+// reads per 24 MFMAs instead of 8 per 12) and ONE register staging set — its
+// 128 accumulators leave no room for a second.  A (fp32 activations) is split into
 // hi/lo bf16 while staging; W is pre-split on the host.  LDS rows are
 // 32 bf16 + 8 pad (80 B): the 16-byte fragment reads (row = lane&31,
 // k = 16 s + 8 (lane>>5)) hit 16 distinct slots per ds_read_b128 group.
@@ -260,7 +260,7 @@ void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo,
 int conv_gemm_x3_block_rows(const ConvGemmArgs& p, int variant) {
   if (p.N % 64 != 0 || (p.gcols && p.gcols % 64 != 0)) return 128;
   if (p.gcols || p.N % 128 != 0) return 128;
-  return (variant == 1 || variant == 4 || variant == 5) ? 256 : 128;
+  return (variant == 1 || variant == 4 || variant == 5 || variant == 6) ? 256 : 128;
 }
 
 namespace {
@@ -294,7 +294,7 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
   if (p.colsum) {
     const int bm = conv_gemm_x3_block_rows(p, variant);
     WSP_CHECK(!p.seg && !p.row_bias && !p.conv2d && p.T >= bm && (variant == 1 || variant == 3 || variant == 4 ||
-                                                                  variant == 5 || variant == 0),
+                                                                  variant == 5 || variant == 6 || variant == 0),
               "conv_gemm_x3: column sums need a uniform batch with T >= block rows and no row bias");
   }
   WSP_CHECK(p.Kp % 64 == 0, "conv_gemm_x3: packed K must be a multiple of 64");
@@ -312,12 +312,15 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
     launch_x3_tile<2, 2, 2, 2, true>(p, h, l, s);  // 128 x 128, 4 waves, swizzled rows: 2 blocks / CU
   } else if (variant == 4) {
     launch_x3_tile<4, 2, 2, 2, true>(p, h, l, s);  // 256 x 128, 8 waves, swizzled rows
-  } else if (variant == 5) {
-    // 256 x 256 only for deep contractions: in-model it wins at K = 3072 (ECAPA conv_cat
-    // -7 %, HuBERT fc2 -13 %) and loses at K <= 1536 (fc1 +19 %, C x C +5 %): its
-    // fewer, longer blocks pay a bigger per-block prologue / epilogue and grid tail
-    if (p.N % 256 == 0 && !p.gcols && p.Kp >= 2048)
-      launch_x3_tile<4, 2, 2, 4, true, 1>(p, h, l, s);  // 256 x 256, 8 waves (4 x 2), 64 x 128 per wave
+  } else if (variant == 5 || variant == 6) {
+    // 256 x 256 (8 waves 4 x 2, 64 x 128 per wave) where N allows it — except short
+    // contractions with the GELU epilogue: 128 erf evaluations per lane at the end of a
+    // K <= 1536 block cost more than the wider tile saves (HuBERT fc1 +13 %, CNN +2 %);
+    // in-model C x C -4 %, conv_cat -15 %, HuBERT fc2 -13 %, out_proj -10 %.
+    // Variant 6 forces the wide tile wherever N allows (experiments).
+    const bool wide = p.N % 256 == 0 && !p.gcols && (variant == 6 || p.act != kActGelu || p.Kp >= 2048);
+    if (wide)
+      launch_x3_tile<4, 2, 2, 4, true, 1>(p, h, l, s);
     else
       launch_x3_tile<4, 2, 2, 2, true>(p, h, l, s);  // variant 4
   } else {

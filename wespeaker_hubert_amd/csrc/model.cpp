@@ -206,7 +206,7 @@ void Model::set_option(const std::string& key, int value) {
     impl->m_ch = value;
     impl->build_simam_params();
   } else if (key == "x3_variant") {
-    WSP_CHECK(value >= 0 && value <= 5, "x3_variant must be 0..5");
+    WSP_CHECK(value >= 0 && value <= 6, "x3_variant must be 0..6");
     impl->x3_variant = value;
   } else {
     throw InvalidArg{"unknown option " + key};
