@@ -71,7 +71,7 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
     m.ecapa = false;
     m.simam = true;
     m.bottleneck = false;
-    m.x3_variant = 3;
+    m.x3_variant = 5;  // MFMA-bound 3x3 convs (K = 9C): wide tiles where N % 256 == 0 (+6 % over variant 3)
     m.m_ch = 64;
     const int nb34[4] = {3, 4, 6, 3}, nb100[4] = {6, 16, 24, 3};
     for (int i = 0; i < 4; ++i) m.nblocks[i] = arch == "SimAM_ResNet34_ASP" ? nb34[i] : nb100[i];
