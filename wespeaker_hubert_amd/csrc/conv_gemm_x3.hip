@@ -312,17 +312,23 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
     launch_x3_tile<2, 2, 2, 2, true>(p, h, l, s);  // 128 x 128, 4 waves, swizzled rows: 2 blocks / CU
   } else if (variant == 4) {
     launch_x3_tile<4, 2, 2, 2, true>(p, h, l, s);  // 256 x 128, 8 waves, swizzled rows
-  } else if (variant == 5 || variant == 6) {
+  } else if (variant == 5) {
     // 256 x 256 (8 waves 4 x 2, 64 x 128 per wave) where N allows it — except short
     // contractions with the GELU epilogue: 128 erf evaluations per lane at the end of a
     // K <= 1536 block cost more than the wider tile saves (HuBERT fc1 +13 %, CNN +2 %);
     // in-model C x C -4 %, conv_cat -15 %, HuBERT fc2 -13 %, out_proj -10 %.
-    // Variant 6 forces the wide tile wherever N allows (experiments).
-    const bool wide = p.N % 256 == 0 && !p.gcols && (variant == 6 || p.act != kActGelu || p.Kp >= 2048);
+    const bool wide = p.N % 256 == 0 && !p.gcols && (p.act != kActGelu || p.Kp >= 2048);
     if (wide)
       launch_x3_tile<4, 2, 2, 4, true, 1>(p, h, l, s);
     else
       launch_x3_tile<4, 2, 2, 2, true>(p, h, l, s);  // variant 4
+  } else if (variant == 6) {
+    // experiments: the 256 x 256 tile wherever N allows (16 waves of 64 x 64 instead
+    // would cap at 128 VGPRs and spill ~300 B in the k-loop)
+    if (p.N % 256 == 0 && !p.gcols)
+      launch_x3_tile<4, 2, 2, 4, true, 1>(p, h, l, s);
+    else
+      launch_x3_tile<4, 2, 2, 2, true>(p, h, l, s);
   } else {
     launch_x3_tile<2, 2, 2, 2>(p, h, l, s);  // 128 x 128, 4 waves
   }
