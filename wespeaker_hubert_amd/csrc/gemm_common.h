@@ -201,13 +201,18 @@ struct ALoader2D {
 // s_memtime stamps) — and a row's byte offset is the tile's base plus a
 // compile-time row step times 4*ldo (no per-element multiply).  Rows >= M get
 // out-of-range buffer offsets: loads return 0, stores are dropped.
-template <int TM, int TN, int ACT, bool RB, bool CS = false>
+template <int TM, int TN, int ACT, bool RB, bool CS = false, bool RES = false>
 __device__ __forceinline__ void gemm_epilogue_store(const ConvGemmArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0,
                                                     int wm, int wn, int lane, double (*cs)[2] = nullptr) {
   const int r32 = lane & 31;
   const int h = lane >> 5;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
   const int ldo4 = p.ldo * 4;
+  // RES: the residual is read per 32-row tile right where it is added (the 16 loads
+  // of a tile are independent and issue together) — no residual register file next
+  // to the accumulators, which wide wave tiles cannot afford
+  const __amdgpu_buffer_rsrc_t rres = make_rsrc(RES ? p.res : p.out);
+  const int ldr4 = p.ldres * 4;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + (wn * TN + j) * 32 + r32;
@@ -227,10 +232,21 @@ __device__ __forceinline__ void gemm_epilogue_store(const ConvGemmArgs& p, f32x1
         const int next = (m0 / p.T + 1) * p.T;
         if (t0 + 32 <= p.M) mode = t0 + 32 <= next ? 0 : (t0 >= next ? 1 : 2);
       }
+      float rv[16];
+      if constexpr (RES) {
+        const int rbase = row0 * ldr4 + col * 4;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rr = (r & 3) + 8 * (r >> 2);
+          rv[r] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rres, rr < lim ? rbase + rr * ldr4 : kOOB, 0, 0));
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rr = (r & 3) + 8 * (r >> 2);
         float y = acc[i][j][r] + bv;
+        if constexpr (RES) y += rv[r];
         if constexpr (RB) {
           const int row = row0 + rr;
           const int rowc = row < p.M ? row : p.M - 1;
@@ -294,40 +310,6 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
                                               int wm, int wn, int lane, unsigned char* smem = nullptr) {
   const int r32 = lane & 31;
   const int h = lane >> 5;
-  if (p.res) {
-    // every residual load of the wave's tiles issued before the first add: one
-    // HBM round trip per block instead of TM (the k-loop's staging registers are
-    // dead here, so TM*TN*16 values fit under the main loop's register peak)
-    // (waves with more than 4 tiles: 4 tiles' worth at a time)
-    const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res);
-    const int ldr4 = p.ldres * 4;
-    constexpr int TMG = (TM * TN <= 4) ? TM : (4 / TN > 0 ? 4 / TN : 1);  // tile rows per group
-#pragma unroll
-    for (int i0 = 0; i0 < TM; i0 += TMG) {
-      float rv[TMG][TN][16];
-#pragma unroll
-      for (int ii = 0; ii < TMG; ++ii) {
-        const int row0 = m0 + (wm * TM + i0 + ii) * 32 + 4 * h;
-        const int lim = p.M - row0;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int base = row0 * ldr4 + (n0 + (wn * TN + j) * 32 + r32) * 4;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int q = (r & 3) + 8 * (r >> 2);
-            const int off = q < lim ? base + q * ldr4 : kOOB;
-            rv[ii][j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, off, 0, 0));
-          }
-        }
-      }
-#pragma unroll
-      for (int ii = 0; ii < TMG; ++ii)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i0 + ii][j][r] += rv[ii][j][r];
-    }
-  }
   if constexpr (WM > 0) {
     if (p.colsum) {  // fused per-utterance column sums (host: uniform batch, T >= BM, no row bias)
       double cs[TN][2];
@@ -342,6 +324,15 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
       gemm_colsum_reduce<TN, WM, WN, WM * TM * 32>(p, cs, m0, n0, wm, wn, lane, smem);
       return;
     }
+  }
+  if (p.res) {  // residual convs: no row bias / column sums (checked on the host)
+    switch (p.act) {
+      case kActRelu: gemm_epilogue_store<TM, TN, kActRelu, false, false, true>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActTanh: gemm_epilogue_store<TM, TN, kActTanh, false, false, true>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActGelu: gemm_epilogue_store<TM, TN, kActGelu, false, false, true>(p, acc, m0, n0, wm, wn, lane); break;
+      default: gemm_epilogue_store<TM, TN, kActNone, false, false, true>(p, acc, m0, n0, wm, wn, lane); break;
+    }
+    return;
   }
   if (p.row_bias) {
     switch (p.act) {
@@ -393,6 +384,7 @@ inline void check_conv_args(const ConvGemmArgs& p, const char* who) {
   for (int i = 0; i < 3; ++i) WSP_CHECK(p.lda[i] % 4 == 0, w + ": lda must be a multiple of 4");
   if (!p.conv2d) WSP_CHECK(p.stride >= 1 && p.Ti >= 1, w + ": call normalized() first");
   if (p.seg) WSP_CHECK(!p.conv2d && p.nseg >= 1 && (p.iseg || p.stride == 1), w + ": segmented batch needs a 1-D conv (input offsets when strided)");
+  WSP_CHECK(!p.res || (!p.row_bias && !p.colsum), w + ": a residual epilogue has no row bias / column sums");
   if (p.gcols) {
     WSP_CHECK(p.amode == kACat && p.cseg[1] == p.cin && !p.conv2d, w + ": grouped conv needs one 1-D segment");
     WSP_CHECK(p.N % p.gcols == 0 && p.gcols % 32 == 0 && p.gcin % 4 == 0, w + ": bad grouped-conv columns");
