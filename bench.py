@@ -35,7 +35,7 @@ HBM_PEAK_GBPS = 8000.0
 def x3_tile(variant, N: int, K: int, gelu: bool = False):
     """(template prefix, BM, BN, threads) of the bf16x3 block launch_conv_gemm_x3 picks."""
     v = 5 if variant is None else variant
-    if (v == 6 or (v == 5 and (not gelu or K >= 2048))) and N % 256 == 0:
+    if v in (5, 6) and N % 256 == 0:
         return "ILi4ELi2ELi2ELi4E", 256, 256, 512
     if v in (1, 4, 5, 6):
         return "ILi4ELi2ELi2ELi2E", 256, 128, 512

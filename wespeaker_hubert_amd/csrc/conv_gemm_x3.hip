@@ -313,18 +313,16 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
   } else if (variant == 4) {
     launch_x3_tile<4, 2, 2, 2, true>(p, h, l, s);  // 256 x 128, 8 waves, swizzled rows
   } else if (variant == 5) {
-    // 256 x 256 (8 waves 4 x 2, 64 x 128 per wave) where N allows it — except short
-    // contractions with the GELU epilogue: 128 erf evaluations per lane at the end of a
-    // K <= 1536 block cost more than the wider tile saves (HuBERT fc1 +13 %, CNN +2 %);
-    // in-model C x C -4 %, conv_cat -15 %, HuBERT fc2 -13 %, out_proj -10 %.
-    const bool wide = p.N % 256 == 0 && !p.gcols && (p.act != kActGelu || p.Kp >= 2048);
-    if (wide)
+    // 256 x 256 (8 waves 4 x 2, 64 x 128 per wave) wherever N allows it: in-model C x C
+    // -10 %, conv_cat -15 %, HuBERT fc1 -18 %, fc2 -20 %, CNN -12 % vs 256 x 128 (with the
+    // per-tile residual epilogue and the A&S GELU; the libm erff made fc1's epilogue lose)
+    if (p.N % 256 == 0 && !p.gcols)
       launch_x3_tile<4, 2, 2, 4, true, 1>(p, h, l, s);
     else
       launch_x3_tile<4, 2, 2, 2, true>(p, h, l, s);  // variant 4
   } else if (variant == 6) {
-    // experiments: the 256 x 256 tile wherever N allows (16 waves of 64 x 64 instead
-    // would cap at 128 VGPRs and spill ~300 B in the k-loop)
+    // experiments slot (now the same tiles as 5; a 16-wave 64 x 64 form of the wide tile
+    // caps registers at 128 and spilled ~300 B per lane in the k-loop)
     if (p.N % 256 == 0 && !p.gcols)
       launch_x3_tile<4, 2, 2, 4, true, 1>(p, h, l, s);
     else
