@@ -192,21 +192,6 @@ struct ALoader2D {
   }
 };
 
-// GELU (exact erf form, fairseq / torch default) with erf from Abramowitz & Stegun
-// 7.1.26 (|error| <= 1.5e-7, ~2.5 fp32 ulp near 1): one exp, one reciprocal and five
-// FMAs instead of the libm erff's branchy rational approximations — the GELU epilogue
-// of a 256-column wave tile evaluates 128 of them per lane.
-__device__ __forceinline__ float gelu_as(float y) {
-  const float x = fabsf(y) * 0.70710678118654752f;
-  const float t = __frcp_rn(fmaf(0.3275911f, x, 1.f));
-  float q = fmaf(1.061405429f, t, -1.453152027f);
-  q = fmaf(q, t, 1.421413741f);
-  q = fmaf(q, t, -0.284496736f);
-  q = fmaf(q, t, 0.254829592f);
-  const float e = 1.f - q * t * __expf(-x * x);  // erf(|y| / sqrt 2)
-  return 0.5f * y * (1.f + copysignf(e, y));
-}
-
 // Shared GEMM epilogue for a wave's TM x TN tiles of 32x32 accumulators
 // (gfx950 32x32 C/D map: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)).
 //   y = act(acc + bias[n] + row_bias[utt(row)][n] + res[row][n]) * scale[n] + shift[n]

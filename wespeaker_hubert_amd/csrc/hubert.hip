@@ -19,12 +19,13 @@ namespace wsp {
 
 namespace {
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// GELU: gelu_as (common.h, A&S 7.1.26 erf, |err| <= 2e-7) — conv0 evaluates one per output
+__device__ __forceinline__ float gelu_erf(float x) { return gelu_as(x); }
 
 // ---------------------------------------------------------------- conv0 ---
 constexpr int kC0 = 512, kK0 = 10, kS0 = 5, kTC = 128;
 
-// PASS 0: stats[0][b][c] += sum_t y;  PASS 1: stats[1][b][c] += sum_t (y - mean)^2;
+// PASS 0: stats[0][b][c] += sum_t y, stats[1][b][c] += sum_t y^2 (f64);
 // PASS 2: out = GELU(GroupNorm(y)).  One thread per channel, one block per
 // (128-frame chunk, utterance); the waveform chunk is staged in LDS and read
 // as a broadcast.
@@ -54,29 +55,32 @@ __global__ __launch_bounds__(kC0) void conv0_kernel(const float* __restrict__ wa
   const int nt = min(kTC, T0 - t0);
   double* s0 = stats + (size_t)b * kC0 + c;
   double* s1 = stats + (size_t)(B + b) * kC0 + c;
-  float mean = 0.f, scale = 1.f, shift = 0.f;
-  if (PASS >= 1) mean = (float)(*s0 / T0);
+  // PASS 0: first and second moments in f64 (one conv pass: var = E[y^2] - mean^2,
+  // exact enough in f64 for fp32 outputs); PASS 2: normalise + affine + GELU + store.
+  float scale = 1.f, shift = 0.f;
   if (PASS == 2) {
-    const float rstd = (float)(1.0 / sqrt(*s1 / T0 + 1e-5));
+    const double m = *s0 / T0;
+    const double var = fmax(*s1 / T0 - m * m, 0.0);
+    const float rstd = (float)(1.0 / sqrt(var + 1e-5));
     scale = rstd * gamma[c];
-    shift = beta[c] - mean * scale;
+    shift = beta[c] - (float)m * scale;
   }
-  float acc = 0.f;
+  double acc = 0.0, acc2 = 0.0;
   for (int t = 0; t < nt; ++t) {
     float y = 0.f;
 #pragma unroll
     for (int k = 0; k < kK0; ++k) y = fmaf(wr[k], xs[t * kS0 + k], y);
     if (PASS == 0) {
-      acc += y;
-    } else if (PASS == 1) {
-      const float d = y - mean;
-      acc = fmaf(d, d, acc);
+      acc += (double)y;
+      acc2 = fma((double)y, (double)y, acc2);
     } else {
       out[(obase + t0 + t) * kC0 + c] = gelu_erf(fmaf(y, scale, shift));
     }
   }
-  if (PASS == 0) atomicAdd(s0, (double)acc);
-  if (PASS == 1) atomicAdd(s1, (double)acc);
+  if (PASS == 0) {
+    atomicAdd(s0, acc);
+    atomicAdd(s1, acc2);
+  }
 }
 
 // ------------------------------------------------------------ layernorm ---
@@ -364,8 +368,6 @@ void launch_hubert_conv0(const float* wav, int B, int N, int ldw, int T0, const 
   WSP_HIP(hipMemsetAsync(stats, 0, sizeof(double) * 2 * B * kC0, s));
   const dim3 grid((T0 + kTC - 1) / kTC, B);
   hipLaunchKernelGGL(conv0_kernel<0>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B, wseg,
-                     oseg);
-  hipLaunchKernelGGL(conv0_kernel<1>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B, wseg,
                      oseg);
   hipLaunchKernelGGL(conv0_kernel<2>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B, wseg,
                      oseg);
