@@ -217,19 +217,44 @@ void launch_frame_stats(const float* x, int ldx, int B, int T, int C, float* out
 }
 
 // --------------------------------------------------------- residual scale ---
+// out = x + h * g[utt]: HBM-bound (2 reads + 1 write per element).  A thread owns
+// one 4-channel column for a run of rows (no per-element 64-bit index division:
+// the utterance is decoded once per row), four rows in flight per step.
 namespace {
+constexpr int kRSRows = 64;  // rows per workgroup
+
 __global__ __launch_bounds__(256) void residual_scale_kernel(const f32x4* __restrict__ x,
                                                              const f32x4* __restrict__ h,
                                                              const float* __restrict__ g,
-                                                             f32x4* __restrict__ out, long n4,
-                                                             int T, int C4, const int* __restrict__ seg,
-                                                             int nseg) {
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    const long row = i / C4;
-    const int c4 = (int)(i - row * C4);
-    const int b = seg ? seg_of(seg, nseg, (int)row) : (int)(row / T);
-    const f32x4 gv = *reinterpret_cast<const f32x4*>(g + ((long)b * C4 + c4) * 4);
-    out[i] = x[i] + h[i] * gv;
+                                                             f32x4* __restrict__ out, int M, int T, int C4,
+                                                             const int* __restrict__ seg, int nseg) {
+  const int tpr = min(C4, 256);             // threads per row
+  const int rpp = 256 / tpr;                // rows per pass
+  const int sub = threadIdx.x / tpr;
+  const int r0 = blockIdx.x * kRSRows;
+  const int r1 = min(M, r0 + kRSRows);
+  for (int c4 = threadIdx.x % tpr; c4 < C4; c4 += tpr) {
+    int r = r0 + sub;
+    for (; r + 3 * rpp < r1; r += 4 * rpp) {
+      f32x4 xv[4], hv[4], gv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int row = r + u * rpp;
+        const int b = seg ? seg_of(seg, nseg, row) : row / T;
+        const long i = (long)row * C4 + c4;
+        xv[u] = x[i];
+        hv[u] = h[i];
+        gv[u] = *reinterpret_cast<const f32x4*>(g + ((long)b * C4 + c4) * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) out[(long)(r + u * rpp) * C4 + c4] = xv[u] + hv[u] * gv[u];
+    }
+    for (; r < r1; r += rpp) {
+      const int b = seg ? seg_of(seg, nseg, r) : r / T;
+      const long i = (long)r * C4 + c4;
+      const f32x4 gv = *reinterpret_cast<const f32x4*>(g + ((long)b * C4 + c4) * 4);
+      out[i] = x[i] + h[i] * gv;
+    }
   }
 }
 }  // namespace
@@ -237,12 +262,13 @@ __global__ __launch_bounds__(256) void residual_scale_kernel(const f32x4* __rest
 void launch_residual_scale(const float* x, const float* h, const float* g, float* out, int B,
                            int T, int C, hipStream_t s, const int* seg, int M) {
   WSP_CHECK(C % 4 == 0, "residual_scale: C % 4");
-  const long n4 = (long)(seg ? M : B * T) * C / 4;
-  if (n4 == 0) return;
-  const int grid = (int)std::min<long>(ceil_div((int)std::min<long>(n4, 1L << 30), 256), 256 * 16);
-  hipLaunchKernelGGL(residual_scale_kernel, dim3(grid), dim3(256), 0, s,
+  const int C4 = C / 4;
+  WSP_CHECK(C4 % 256 == 0 || 256 % C4 == 0, "residual_scale: C/4 must divide or be a multiple of 256");
+  const int rows = seg ? M : B * T;
+  if (rows == 0) return;
+  hipLaunchKernelGGL(residual_scale_kernel, dim3(ceil_div(rows, kRSRows)), dim3(256), 0, s,
                      reinterpret_cast<const f32x4*>(x), reinterpret_cast<const f32x4*>(h), g,
-                     reinterpret_cast<f32x4*>(out), n4, T, C / 4, seg, B);
+                     reinterpret_cast<f32x4*>(out), rows, T, C4, seg, B);
   WSP_HIP(hipGetLastError());
 }
 
