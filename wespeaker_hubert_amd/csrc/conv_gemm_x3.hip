@@ -305,7 +305,7 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
   } else if (p.gcols) {
     // grouped (HuBERT pos_conv: 16 groups x 64 padded columns, K = 48 x 128): 256-row
     // blocks halve the per-row re-reads of the group's 1.5 MB weight slice
-    if (variant == 5) launch_x3_tile<8, 1, 1, 2>(p, h, l, s);
+    if (variant == 5) launch_x3_tile<8, 1, 1, 2, true>(p, h, l, s);
     else launch_x3_tile<4, 1, 1, 2>(p, h, l, s);  // blocks stay inside one group
   } else if (p.N % 128 != 0) {
     launch_x3_tile<4, 1, 1, 2>(p, h, l, s);  // 128 x 64, 4 waves
