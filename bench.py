@@ -7,12 +7,18 @@ batch, all in libwsp_hip.so.  Multi-GPU: one rank per GPU (torchrun), each
 rank extracts its own shard (weak scaling, no data-path collective).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+
+`--gpus N` without a torchrun environment starts N ranks itself (torchrun as a
+child process, before anything touches the GPU) and relays rank 0's line;
+under torchrun WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -150,7 +156,87 @@ def parse():
     ap.add_argument("--precision", type=int, default=1, help="1 = bf16x3 split MFMA, 0 = f32 MFMA")
     ap.add_argument("--x3-variant", type=int, default=None)
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing pass")
+    ap.add_argument("--no-f32", action="store_true", help="skip the exact-f32 (precision 0) side measurement")
+    ap.add_argument("--sustain-seconds", type=float, default=2.0,
+                    help="extra untimed-for-value window reported as value_sustained (>= this many seconds)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU/gloo rehearsal of the rank launch, barriers and JSON (no GPU work; tests only)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(gpus: int) -> int:
+    """One process per GPU, as the driver's own torchrun line does (and as
+    tools/extract_embedding.sh:40-63 starts one extractor per GPU): a child
+    torchrun, started before any GPU call in this process; rank 0 prints the
+    JSON line, which reaches our stdout directly."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def plumbing_main(args):
+    """--plumbing: the multi-rank skeleton of main() on CPU (gloo) with a
+    sleep as the step, so tests can check the launch / max-over-ranks / JSON
+    contract without a GPU."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if world > 1:
+        dist.init_process_group("gloo")
+    B = args.batch or 256
+    for _ in range(args.warmup):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.002 * (1 + rank))
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "embeddings/sec on 5s 16kHz utts (plumbing rehearsal, no GPU work)",
+                          "value": round(world * B * args.steps / el, 2), "unit": "emb/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / args.steps * 1e3, 3), "scaling": "weak",
+                          "config": {"batch_per_gpu": B, "global_batch": B * world,
+                                     "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: the CPUs this process may actually use
+    (BASELINE.md §3 asks for os.cpu_count(); on the GPU box os.cpu_count() and the
+    affinity mask report the whole host (256) while the cgroup quota
+    (/sys/fs/cgroup/cpu.max) grants 16 CPUs -- 256 threads on 16 CPUs ran the
+    oracle 200x slower, so the quota caps the count)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(-(-int(quota) // int(period)))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
 
 
 def cpu_baseline(arch: str, sd, num_samples: int, budget_s: float):
@@ -158,7 +244,7 @@ def cpu_baseline(arch: str, sd, num_samples: int, budget_s: float):
     CMN, then the fp32 PyTorch-CPU restatement of the reference ECAPA forward.
     Bounded sample: batches of 8 utterances until >= budget_s of work."""
     from oracle import fbank_ref, models_ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
 
@@ -176,7 +262,7 @@ def cpu_baseline(arch: str, sd, num_samples: int, budget_s: float):
         el = time.perf_counter() - t0
         if el >= budget_s or done >= 256:
             break
-    return {"value": done / el, "unit": "emb/s", "cores": threads, "kind": "port",
+    return {"value": done / el, "unit": "emb/s", "cores": threads, "kind": "port", "os_cpu_count": os.cpu_count(),
             "sample": f"{done} synthetic {num_samples / 16000:.0f}s utts, batches of 8, "
                       f"numpy-f64 fbank + torch-CPU fp32 {arch} (oracle restatement), {el:.1f}s"}
 
@@ -185,7 +271,7 @@ def cpu_baseline_hubert(sd_fe, sd, num_samples: int, budget_s: float):
     """Oracle ('port') C4 chain on the host cores: fp32 torch-CPU HuBERT-base +
     s3prl glue + CMN + ECAPA_TDNN_GLOB_c512.  Bounded sample: batches of 2."""
     from oracle import hubert_ref, models_ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     sdf = {k: torch.from_numpy(v) for k, v in sd_fe.items()}
     sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
@@ -204,16 +290,22 @@ def cpu_baseline_hubert(sd_fe, sd, num_samples: int, budget_s: float):
         el = time.perf_counter() - t0
         if el >= budget_s or done >= 64:
             break
-    return {"value": done / el, "unit": "emb/s", "cores": threads, "kind": "port",
+    return {"value": done / el, "unit": "emb/s", "cores": threads, "kind": "port", "os_cpu_count": os.cpu_count(),
             "sample": f"{done} synthetic {num_samples / 16000:.0f}s utts, batches of 2, torch-CPU fp32 "
                       f"HuBERT-base + s3prl glue + CMN + ECAPA_TDNN_GLOB_c512 (oracle restatement), {el:.1f}s"}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if args.plumbing:
+        return plumbing_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -290,6 +382,40 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     value = world * B * args.steps / el
+
+    def timed(n):
+        barrier()
+        t = time.perf_counter()
+        for _ in range(n):
+            step()
+        barrier()
+        e = time.perf_counter() - t
+        if dist is not None:
+            tt = torch.tensor([e], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            e = float(tt.item())
+        return e
+
+    # sustained window (>= --sustain-seconds of back-to-back steps, profiling
+    # off): the same step count on every rank, derived from the max-over-ranks time
+    sustained = None
+    if args.sustain_seconds > 0:
+        n_s = max(args.steps, int(np.ceil(args.sustain_seconds / (el / args.steps))))
+        e_s = timed(n_s)
+        sustained = {"value": round(world * B * n_s / e_s, 2), "steps": n_s, "seconds": round(e_s, 3),
+                     "ms_per_step": round(e_s / n_s * 1e3, 3)}
+    # exact-f32 MFMA (precision 0) beside the bf16x3 headline
+    exact = None
+    if args.precision == 1 and not args.no_f32:
+        for mm in (model, fe):
+            if mm is not None:
+                mm.set_option("precision", 0)
+                mm.to(dev)
+        step()
+        n_f = max(2, args.steps // 4)
+        e_f = timed(n_f)
+        exact = {"value": round(world * B * n_f / e_f, 2), "steps": n_f,
+                 "ms_per_step": round(e_f / n_f * 1e3, 3), "dtype": "f32 (v_mfma_f32_32x32x2_f32)"}
 
     kernels, roof = {}, None
     if not args.no_profile:
@@ -404,7 +530,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32 (bf16x3 split MFMA, fp32 accumulate)" if args.precision == 1 else "f32",
+        "value_sustained": sustained,
+        "value_exact_f32": exact,
         "data": ("synthetic (clip(N(0,0.1)) [-1,1] audio, seeded random-init weights)" if hubert else
                  "synthetic (clip(N(0,0.1)) x32768 PCM16-valued audio, seeded random-init weights)"),
         "config": {"workload": (f"HuBERT-base (s3prl featurizer) + CMN + ECAPA_TDNN_GLOB_c512 extract, "

@@ -152,7 +152,8 @@ int wsp_model_profile_query(wsp_model* m, const char* kernel_class, int* launche
  * bin/extract.py:104-106's apply_cmvn (cmn = 1).  Handles come from
  * wsp_model_create("HuBERT_base", 1, 768, 0, 0, &m); parameters are the
  * reference checkpoint's "frontend.*" entries. */
-/* Frames per utterance: len(range(0, num_samples, 320)). num_samples >= 400. */
+/* Frames per utterance: len(range(0, num_samples, 320)). num_samples >= 1; inputs
+ * shorter than 800 samples run zero-padded to 800 (s3prl MIN_SECOND = 0.05 s). */
 int wsp_frontend_out_frames(const wsp_model* m, int num_samples, int* frames);
 int wsp_frontend_workspace_bytes(const wsp_model* m, int B, int num_samples, size_t* bytes);
 /* wav [B][num_samples] f32 in [-1, 1] (bin/extract.py:100-102: not x32768)
@@ -161,7 +162,7 @@ int wsp_frontend_forward(wsp_model* m, const float* wav, int B, int num_samples,
                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* Ragged batch: B whole utterances concatenated in `wav` (device), utterance b =
- * num_samples[b] samples (HOST int32 array, each >= 400) -> feats rows
+ * num_samples[b] samples (HOST int32 array, each >= 1) -> feats rows
  * [frame_offsets[b], frame_offsets[b+1]) of [sum_b ceil(num_samples[b]/320)][768]
  * (frame_offsets: HOST int32 [B+1] output, may be NULL).  Each utterance's rows
  * equal its batch-of-one result (conv padding, attention, length match, CMN per

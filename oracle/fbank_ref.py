@@ -26,6 +26,9 @@ float64 direct-DFT formulation) in tests.
 """
 from __future__ import annotations
 
+import functools
+import math
+
 import numpy as np
 
 FLT_EPS = np.float32(np.finfo(np.float32).eps)
@@ -37,25 +40,42 @@ def mel_scale(f):
 
 def mel_banks(num_bins=80, padded=512, sample_freq=16000.0, low_freq=20.0, high_freq=0.0,
               dtype=np.float32) -> np.ndarray:
-    """get_mel_banks (torchaudio kaldi.py) — (num_bins, padded//2 + 1) incl. zero Nyquist column."""
+    return _mel_banks(num_bins, padded, sample_freq, low_freq, high_freq).astype(dtype)
+
+
+@functools.lru_cache(maxsize=8)
+def _mel_banks(num_bins, padded, sample_freq, low_freq, high_freq) -> np.ndarray:
+    """torchaudio's get_mel_banks arithmetic: python-double mel_low / delta
+    scalars cast to float32, float32 tensor ops in torchaudio's order (checked
+    against torch's own evaluation, which promotes exactly like this).  The one
+    transcendental, the float32 log of (1 + f / 700), is taken correctly rounded:
+    torch's CPU float32 log is host-dependent (SLEEF u10 paths), so torchaudio's
+    own filter weights differ between machines by up to 7e-6 (measured: this
+    container's Xeon vs the GPU box's host, 41 of 501 weights; numpy's float32 log
+    differs again) -- up to 8e-5 in a log-mel value.  This restatement and the
+    kernel's generated table (tools/gen_fbank_mel_table.py) use the correctly
+    rounded value, i.e. glibc logf."""
+    f32 = np.float32
     num_fft_bins = padded // 2
     nyquist = 0.5 * sample_freq
     if high_freq <= 0.0:
         high_freq += nyquist
     fft_bin_width = sample_freq / padded
-    mel_low = 1127.0 * np.log(1.0 + low_freq / 700.0)
-    mel_high = 1127.0 * np.log(1.0 + high_freq / 700.0)
-    delta = (mel_high - mel_low) / (num_bins + 1)
-    b = np.arange(num_bins, dtype=dtype)[:, None]
-    left = (mel_low + b * dtype(delta)).astype(dtype)
-    center = (mel_low + (b + 1) * dtype(delta)).astype(dtype)
-    right = (mel_low + (b + 2) * dtype(delta)).astype(dtype)
-    freq = (dtype(fft_bin_width) * np.arange(num_fft_bins, dtype=dtype))[None, :]
-    mel = (1127.0 * np.log(dtype(1.0) + freq / dtype(700.0))).astype(dtype)
+    mel_low = 1127.0 * math.log(1.0 + low_freq / 700.0)
+    mel_high = 1127.0 * math.log(1.0 + high_freq / 700.0)
+    delta = f32((mel_high - mel_low) / (num_bins + 1))
+    b = np.arange(num_bins, dtype=f32)[:, None]
+    left = f32(mel_low) + b * delta
+    center = f32(mel_low) + (b + f32(1.0)) * delta
+    right = f32(mel_low) + (b + f32(2.0)) * delta
+    x = f32(1.0) + (f32(fft_bin_width) * np.arange(num_fft_bins, dtype=f32)) / f32(700.0)
+    mel = (f32(1127.0) * np.log(x.astype(np.float64)).astype(f32))[None, :]
     up = (mel - left) / (center - left)
     down = (right - mel) / (right - center)
-    w = np.maximum(dtype(0), np.minimum(up, down)).astype(dtype)
-    return np.concatenate([w, np.zeros((num_bins, 1), dtype=dtype)], axis=1)
+    w = np.maximum(f32(0), np.minimum(up, down)).astype(f32)
+    out = np.concatenate([w, np.zeros((num_bins, 1), dtype=f32)], axis=1)
+    out.setflags(write=False)
+    return out
 
 
 def _frames(wave: np.ndarray, frame_len: int, frame_shift: int) -> np.ndarray:
@@ -92,7 +112,11 @@ def fbank(wave, num_mel_bins=80, frame_length_ms=25.0, frame_shift_ms=10.0, samp
     mel = power @ banks.T
     out = np.log(np.maximum(mel, FLT_EPS)).astype(np.float32)
     if cmn:
-        out = (out - out.mean(axis=0, keepdims=True)).astype(np.float32)
+        # speaker.py:102-103 `feat - torch.mean(feat, 0)`: torch's float32 mean
+        # uses cascade summation (~exact); numpy's float32 mean over axis 0 of a
+        # C-contiguous array accumulates naively (~3e-5 off at T = 498), so the
+        # mean is taken in float64 here.
+        out = (out - out.astype(np.float64).mean(axis=0, keepdims=True)).astype(np.float32)
     return out
 
 

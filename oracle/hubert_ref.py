@@ -12,9 +12,15 @@ do_stable_layer_norm=False):
   x + GELU(SamePad(weight-norm grouped conv k128 g16 pad 64)(x)) -> LayerNorm
   12 x post-LN layers: x = LN(x + MHA(x)); x = LN(x + fc2(GELU(fc1(x))))
   hidden states = [input of layer 0] + [output of each layer]  (13)
-s3prl glue restated from s3prl>=0.4 (cannot be verified offline):
-  * S3PRLUpstream length match: every hidden state padded to
-    len(range(0, W, 320)) frames by repeating its last frame;
+s3prl glue restated from s3prl>=0.4 `s3prl/nn/upstream.py` S3PRLUpstream.forward
+(published source; cannot be verified offline), called at
+wespeaker/frontend/s3prl.py:80-82:
+  * MIN_SECOND = 0.05: when the longest waveform is shorter than
+    0.05 * 16000 = 800 samples, the batch is zero-padded to 800 samples BEFORE
+    the upstream (so conv0's GroupNorm sees the padding);
+  * length match: every hidden state is matched to len(range(0, W_padded, 320))
+    frames by repeating its last frame (or trimming), then trimmed to
+    (W_original - 1) // 320 + 1 frames;
   * Featurizer (normalize=False): sum_l softmax(weights)_l * h_l.
 **Parity unpinned against the reference** (s3prl absent, weights download by
 URL).  `hubert_hidden_states` is pinned against transformers' HubertModel
@@ -94,8 +100,23 @@ def match_length(h: Tensor, num_samples: int, downsample_rate: int = 320) -> Ten
     return h[:, :tgt]
 
 
+MIN_SECOND = 0.05     # s3prl/nn/upstream.py
+SAMPLE_RATE = 16000
+
+
+def s3prl_upstream(wav: Tensor, sd: Dict[str, Tensor]) -> List[Tensor]:
+    """S3PRLUpstream.forward on an equal-length batch (B, W): the 13 length-matched
+    hidden states, each (B, len(range(0, W, 320)), 768), with the MIN_SECOND
+    zero pad of short batches."""
+    W = wav.shape[1]
+    min_len = int(MIN_SECOND * SAMPLE_RATE)
+    x = F.pad(wav, (0, min_len - W)) if W < min_len else wav
+    tgt = s3prl_num_frames(W)
+    return [match_length(h, x.shape[1])[:, :tgt] for h in hubert_hidden_states(x, sd)]
+
+
 def s3prl_frontend(wav: Tensor, sd: Dict[str, Tensor]) -> Tensor:
     """S3prlFrontend.forward (multilayer_feature=True, layer=-1, frozen)."""
-    hs = [match_length(h, wav.shape[1]) for h in hubert_hidden_states(wav, sd)]
+    hs = s3prl_upstream(wav, sd)
     w = torch.softmax(sd["frontend.featurizer.weights"], dim=-1)
     return sum(w[i] * h for i, h in enumerate(hs))

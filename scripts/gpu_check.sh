@@ -12,7 +12,7 @@ run() {
   echo "== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
   return $rc
 }
-run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider; rc=$?
+run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread; rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 run bench 600 python bench.py $BENCH_ARGS || exit $?

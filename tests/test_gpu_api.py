@@ -83,7 +83,7 @@ def test_load_model_extract_embedding_list(model_dir, wav_scp):
         assert e.shape == (192,) and e.dtype == np.float32
         ref = _oracle_embed(sd, pcms[n])
         assert _cos(e, ref) >= 0.9999
-        assert np.abs(e - ref).max() < 2e-3  # fbank fp32 rounding propagates (see test_gpu_parity)
+        assert np.abs(e - ref).max() < 1e-4  # waveform -> embedding, north-star per-dim bar
     sim = spk.compute_similarity(scp.replace("wav.scp", "u00.wav"), scp.replace("wav.scp", "u01.wav"))
     e0 = _oracle_embed(sd, pcms["u00"])
     e1 = _oracle_embed(sd, pcms["u01"])

@@ -57,15 +57,14 @@ def test_hidden_state_matches_oracle(sd_np, sd_t, layer):
     fe = _frontend(sd_np, layer=layer, multilayer=False)
     got = fe.extract(torch.from_numpy(wav).to(DEV)).cpu()
     with torch.no_grad():
-        hs = hubert_ref.hubert_hidden_states(torch.from_numpy(wav), sd_t)
-    ref = hubert_ref.match_length(hs[layer], wav.shape[1])
+        ref = hubert_ref.s3prl_upstream(torch.from_numpy(wav), sd_t)[layer]
     assert got.shape == ref.shape == (2, 50, 768)
     d = (got - ref).abs().max().item()
     assert d <= FEAT_ATOL, f"layer {layer}: max |delta| {d}"
 
 
 @pytest.mark.parametrize("precision", [1, 0], ids=["bf16x3", "f32"])
-@pytest.mark.parametrize("W", [16000, 12345, 400, 48000])
+@pytest.mark.parametrize("W", [16000, 12345, 400, 48000, 799, 250, 1])
 def test_featurizer_output_matches_oracle(sd_np, sd_t, precision, W):
     wav = _wav(8, 2, W)
     fe = _frontend(sd_np, precision=precision)
@@ -86,8 +85,23 @@ def test_last_layer_when_not_multilayer(sd_np, sd_t):
     wav = _wav(9, 1, 8000)
     got = _frontend(sd_np, multilayer=False).extract(torch.from_numpy(wav).to(DEV)).cpu()
     with torch.no_grad():
-        ref = hubert_ref.match_length(hubert_ref.hubert_hidden_states(torch.from_numpy(wav), sd_t)[-1], 8000)
+        ref = hubert_ref.s3prl_upstream(torch.from_numpy(wav), sd_t)[-1]
     assert (got - ref).abs().max().item() <= FEAT_ATOL
+
+
+def test_short_input_is_zero_padded_to_min_second(sd_np, sd_t):
+    """s3prl S3PRLUpstream.forward pads batches shorter than MIN_SECOND (800
+    samples) with zeros before HuBERT: the padded samples change the features
+    (GroupNorm / conv frames), and the output keeps len(range(0, W, 320)) frames."""
+    W = 600
+    wav = _wav(14, 2, W)
+    got = _frontend(sd_np).extract(torch.from_numpy(wav).to(DEV)).cpu()
+    with torch.no_grad():
+        ref = hubert_ref.s3prl_frontend(torch.from_numpy(wav), sd_t)
+        padded = hubert_ref.s3prl_frontend(torch.from_numpy(np.pad(wav, ((0, 0), (0, 200)))), sd_t)
+    assert got.shape == (2, 2, 768)
+    assert (got - ref).abs().max().item() <= FEAT_ATOL
+    assert (got - padded[:, :2]).abs().max().item() <= FEAT_ATOL
 
 
 def test_batch_rows_independent_and_chunked(sd_np):
@@ -130,7 +144,7 @@ def test_hubert_ecapa_chain_embeddings(sd_np, sd_t):
 def test_ragged_batch_equals_batch_of_one(sd_np, sd_t, layer, multi):
     """wsp_frontend_forward_segments: utterances of different lengths in one launch
     give each utterance's batch-of-one features (and the oracle's)."""
-    lens = [400, 12345, 16000, 8007, 48000, 1999]
+    lens = [400, 12345, 16000, 8007, 48000, 1999, 250, 700]
     wavs = [_wav(40 + i, 1, n)[0] for i, n in enumerate(lens)]
     fe = _frontend(sd_np, layer=layer, multilayer=multi)
     feats, offs = fe.extract_segments([torch.from_numpy(w) for w in wavs], cmn=True)
@@ -139,12 +153,11 @@ def test_ragged_batch_equals_batch_of_one(sd_np, sd_t, layer, multi):
         one = fe.extract(torch.from_numpy(w[None]).to(DEV), cmn=True)[0]
         got = feats[offs[i]:offs[i + 1]]
         assert (got - one).abs().max().item() <= 1e-5, i
-        if i in (0, 3):
+        if i in (0, 3, 6, 7):
             with torch.no_grad():
                 if layer < 0:
                     ref = hubert_ref.s3prl_frontend(torch.from_numpy(w[None]), sd_t)
                 else:
-                    ref = hubert_ref.match_length(hubert_ref.hubert_hidden_states(torch.from_numpy(w[None]), sd_t)[layer],
-                                                  len(w))
+                    ref = hubert_ref.s3prl_upstream(torch.from_numpy(w[None]), sd_t)[layer]
             ref = _cmn(ref)[0]
             assert (got.cpu() - ref).abs().max().item() <= FEAT_ATOL

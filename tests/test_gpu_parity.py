@@ -1,9 +1,12 @@
 """GPU parity: HIP path (through the C-ABI) vs the CPU oracle and the
 reference golden fixtures.  Tolerances (BASELINE.json north_star):
 embeddings per-dim |delta| < 1e-4 and cosine >= 0.9999 on identical inputs.
-fbank: log-mel |delta| <= 2e-3 max / 3e-5 mean vs the float64 oracle (the
-reference's own float32 torchaudio path deviates from float64 by ~1e-4 on
-low-energy bins; fbank parity vs reference outputs is unpinned, see oracle/).
+fbank: the HIP kernel computes in float64 and must sit within 1e-5 (max
+log-mel) of the float64 oracle AND no further from it than the float32
+restatement of the reference's own torchaudio path (fbank_ref.fbank(dtype=
+float32), 4.8e-6 .. 1.7e-4 on these inputs; parity vs reference outputs is
+unpinned, see oracle/).  Waveform -> embedding chains are held to the same
+per-dim 1e-4 / cosine 0.9999 bar as feature -> embedding.
 """
 import glob
 import os
@@ -148,21 +151,38 @@ def test_ecapa_deterministic():
     np.testing.assert_array_equal(a, b)
 
 
+FBANK_ATOL = 1e-5  # two output ulps at |log-mel| ~ 20
+
+
 @pytest.mark.parametrize("N", [80000, 16123, 400, 561])
 def test_fbank_matches_oracle(N):
     from wespeaker_hubert_amd.frontend import compute_fbank
     wav = synth_audio(11, 3, N)
     got = compute_fbank(torch.from_numpy(wav).to(DEV), scale=1.0, cmn=False).cpu().numpy()
     ref = np.stack([fbank_ref.fbank(w) for w in wav])
+    ref32 = np.stack([fbank_ref.fbank(w, dtype=np.float32) for w in wav])
     assert got.shape == ref.shape
     d = np.abs(got - ref)
-    assert d.max() <= 2e-3 and d.mean() <= 3e-5, (d.max(), d.mean())
-    # CMN + int16 input + dataset-path scaling give the same features
+    err32 = float(np.abs(ref32 - ref).max())
+    # no less accurate than an fp32 Kaldi fbank (+ one output ulp of slack)
+    assert d.max() <= FBANK_ATOL and d.max() <= err32 + 2e-6, (d.max(), err32)
+    # CMN (fused into the fbank launch) + int16 input + dataset-path scaling give the same features
     got_cmn = compute_fbank(torch.from_numpy(wav.astype(np.int16)).to(DEV), scale=1.0, cmn=True).cpu().numpy()
-    ref_cmn = ref - ref.mean(axis=1, keepdims=True)
-    assert np.abs(got_cmn - ref_cmn).max() <= 2e-3
+    ref_cmn = np.stack([fbank_ref.fbank(w, cmn=True) for w in wav])
+    assert np.abs(got_cmn - ref_cmn).max() <= FBANK_ATOL
     got_sc = compute_fbank(torch.from_numpy(wav / 32768.0).float().to(DEV), scale=32768.0, cmn=False).cpu().numpy()
-    assert np.abs(got_sc - ref).max() <= 2e-3
+    assert np.abs(got_sc - ref).max() <= FBANK_ATOL
+
+
+def test_fbank_batch_independent_and_deterministic():
+    """One workgroup per utterance, fixed-order CMN sums: row b of a batch is
+    bit-identical to the batch-of-one result and to a second run."""
+    from wespeaker_hubert_amd.frontend import compute_fbank
+    wav = torch.from_numpy(synth_audio(13, 5, 48000)).to(DEV)
+    a = compute_fbank(wav, cmn=True).cpu().numpy()
+    b = compute_fbank(wav, cmn=True).cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(a[3:4], compute_fbank(wav[3:4], cmn=True).cpu().numpy())
 
 
 def test_fbank_short_input_gives_zero_frames():
@@ -184,7 +204,7 @@ def test_fbank_tone_and_silence():
     # tones: bins far below the peaks have energy ~1e-9 of the peak and fp32
     # FFT noise there; compare where the energy is within 1e6 of the frame max
     mask = ref[0] > ref[0].max(axis=1, keepdims=True) - np.log(1e6)
-    assert np.abs(got[0] - ref[0])[mask].max() <= 2e-3
+    assert np.abs(got[0] - ref[0])[mask].max() <= FBANK_ATOL
 
 
 def test_end_to_end_wave_to_embedding():
@@ -197,10 +217,9 @@ def test_end_to_end_wave_to_embedding():
     with torch.no_grad():
         _, ref = models_ref.forward("ECAPA_TDNN_c512", torch.from_numpy(ref_feats),
                                     {k: torch.from_numpy(v) for k, v in sd.items()})
-    # different fbank rounding (<=2e-3 on a few low-energy bins) propagates;
-    # the embedding still agrees to cosine >= 0.9999
-    assert _cos_rows(emb, ref.numpy()).min() >= EMB_COS
-    # and on identical features the model is exact to 1e-4
+    # waveform in -> embedding out, against the oracle chain: the north-star bar
+    _assert_emb(emb, ref.numpy())
+    # and on identical features
     with torch.no_grad():
         _, ref2 = models_ref.forward("ECAPA_TDNN_c512", feats.cpu(), {k: torch.from_numpy(v) for k, v in sd.items()})
     _assert_emb(emb, ref2.numpy())

@@ -73,3 +73,25 @@ def test_match_length_and_featurizer(sd):
     with torch.no_grad():
         f = s3prl_frontend(wav, sd)
     assert f.shape == (1, s3prl_num_frames(4000), 768) and torch.isfinite(f).all()
+
+
+def test_s3prl_min_second_zero_pad(sd):
+    """S3PRLUpstream.forward (s3prl>=0.4, MIN_SECOND = 0.05): a batch shorter than
+    800 samples runs zero-padded to 800; the output keeps len(range(0, W, 320))
+    frames and equals the explicitly padded input's first frames.  Restated from
+    s3prl's published source: parity unpinned (s3prl is absent offline)."""
+    from oracle.hubert_ref import s3prl_upstream
+    for W in (1, 250, 400, 640, 799):
+        wav = torch.from_numpy(synth_audio(5, 2, W, int16_scale=False))
+        with torch.no_grad():
+            got = s3prl_frontend(wav, sd)
+            pad = s3prl_frontend(torch.nn.functional.pad(wav, (0, 800 - W)), sd)
+            hs = s3prl_upstream(wav, sd)
+        assert got.shape == (2, s3prl_num_frames(W), 768)
+        assert len(hs) == 13 and all(h.shape == got.shape for h in hs)
+        torch.testing.assert_close(got, pad[:, :got.shape[1]], rtol=0, atol=0)
+    # at >= 800 samples nothing is padded
+    wav = torch.from_numpy(synth_audio(6, 1, 800, int16_scale=False))
+    with torch.no_grad():
+        hs = hubert_hidden_states(wav, sd)
+        torch.testing.assert_close(s3prl_upstream(wav, sd)[12], match_length(hs[12], 800), rtol=0, atol=0)

@@ -83,7 +83,7 @@ def _engine_oracle(pcm, sd, samples_per_chunk):
             else:
                 c = np.concatenate([tail, chunks[0][:n - len(tail)]])
             chunks.append(c)
-    x = np.stack([c - c.mean(0, keepdims=True) for c in chunks]).astype(np.float32)
+    x = np.stack([c - c.astype(np.float64).mean(0, keepdims=True) for c in chunks]).astype(np.float32)
     with torch.no_grad():
         _, e = models_ref.forward(ARCH, torch.from_numpy(x), {k: torch.from_numpy(v) for k, v in sd.items()})
     return e.numpy().mean(0)
@@ -121,7 +121,7 @@ def test_gpu_extract_emb_main_matches_engine_oracle(exported, spc):
         e = got[k]
         cos = float(e @ ref / np.linalg.norm(e) / np.linalg.norm(ref))
         assert cos >= 0.9999, (k, cos)
-        assert np.abs(e - ref).max() <= 2e-3 * max(1.0, float(np.abs(ref).max())), k
+        assert np.abs(e - ref).max() < 1e-4, k  # waveform -> embedding, north-star per-dim bar
     # asv_main: (cos + 1) / 2 of the two engine embeddings
     r = subprocess.run([os.path.join(BIN, "asv_main"), "--speaker_model_path", path, "--enroll_wav",
                         str(d / "mid.wav"), "--test_wav", str(d / "long.wav"), "--SamplesPerChunk", str(spc)],

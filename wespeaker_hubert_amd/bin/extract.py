@@ -49,7 +49,7 @@ from ..s3prl_frontend import S3prlFrontend
 from ..speaker_model import get_speaker_model
 from . import _fire
 
-AUDIO_EXT = {"wav"}
+AUDIO_FORMAT_SETS = {"flac", "mp3", "m4a", "ogg", "opus", "wav", "wma"}  # processor.py:34
 
 
 def parse_config_or_kwargs(config_file, **kwargs):
@@ -72,29 +72,28 @@ def iter_raw(lines: List[str]) -> Iterator[Tuple[str, str, list]]:
 
 def decode_raw(item) -> Tuple[str, np.ndarray, int]:
     key, wav, vad = item
-    pcm, sr = audio.load_wav(wav)
-    x = pcm[0]
+    # processor.py:162-168 torchaudio.load(normalize=True); the stream carries the
+    # int16-scale values compute_fbank sees (processor.py:492 `wav * (1 << 15)`)
+    pcm, sr = audio.load_wav(wav, normalize=True)
+    x = pcm[0] * np.float32(1 << 15)
     if vad:  # processor.parse_raw apply_vad: concatenate voiced segments
         x = np.concatenate([x[int(float(s) * sr):int(float(e) * sr)] for s, e in vad])
     return key, x, sr
 
 
 def iter_shard(lines: List[str]) -> Iterator[Tuple[str, np.ndarray, int]]:
-    """processor.tar_file_and_group: files grouped by prefix, audio by extension."""
+    """processor.tar_file_and_group (processor.py:70-110): files grouped by
+    prefix, audio decoded by extension with torchaudio.load's normalize=True
+    scaling (audio.load_audio).  Audio extensions this build cannot decode
+    raise instead of being dropped from the ark."""
     for path in lines:
         with tarfile.open(path, mode="r:*") as tar:
             for ti in tar:
                 prefix, _, ext = ti.name.rpartition(".")
-                if ext in AUDIO_EXT:
+                if ext in AUDIO_FORMAT_SETS:
                     data = tar.extractfile(ti).read()
-                    tmp = io.BytesIO(data)
-                    import wave
-                    with wave.open(tmp, "rb") as w:
-                        sr = w.getframerate()
-                        ch = w.getnchannels()
-                        raw = w.readframes(w.getnframes())
-                    x = np.frombuffer(raw, dtype="<i2").reshape(-1, ch)[:, 0].copy()
-                    yield prefix, x, sr
+                    x, sr = audio.load_audio(data, fmt=ext, normalize=True, name=f"{path}:{ti.name}")
+                    yield prefix, x[0] * np.float32(1 << 15), sr  # int16 scale, as decode_raw
 
 
 def get_random_chunk(data: np.ndarray, chunk_len: int, rng: random.Random) -> np.ndarray:

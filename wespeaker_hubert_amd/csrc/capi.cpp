@@ -18,19 +18,19 @@ void set_error(const std::string& m) { g_err = m; }
 const std::string& get_error() { return g_err; }
 
 // fbank tables, one device copy per device
-static const float* fbank_tables_dev() {
+static const double* fbank_tables_dev() {
   static std::mutex mu;
-  static std::vector<float*> per_dev;
+  static std::vector<double*> per_dev;
   int dev = 0;
   WSP_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(mu);
   if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1, nullptr);
   if (!per_dev[dev]) {
-    std::vector<float> h(kFbankTableFloats);
+    std::vector<double> h(kFbankTableDoubles);
     fbank_tables(h.data());
-    float* d = nullptr;
-    WSP_HIP(hipMalloc(&d, h.size() * sizeof(float)));
-    WSP_HIP(hipMemcpy(d, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    double* d = nullptr;
+    WSP_HIP(hipMalloc(&d, h.size() * sizeof(double)));
+    WSP_HIP(hipMemcpy(d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
     per_dev[dev] = d;
   }
   return per_dev[dev];

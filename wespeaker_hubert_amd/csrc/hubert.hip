@@ -339,19 +339,21 @@ __global__ __launch_bounds__(256) void mha_kernel(const float* __restrict__ qkv,
 // 256-B row segments, partial sums combined through LDS.
 __global__ __launch_bounds__(256) void cmn_rows_kernel(float* __restrict__ x, int T_, int D,
                                                        const int* __restrict__ seg) {
-  __shared__ float part[4][64];
+  // f64 partial sums in a fixed order (torch's float32 mean is cascade-summed,
+  // i.e. ~exact; a plain f32 running sum drifts ~1e-5 at a few hundred frames)
+  __shared__ double part[4][64];
   const int b = blockIdx.y, c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
   const int T = seg ? seg[b + 1] - seg[b] : T_;
   float* p = x + (seg ? (size_t)seg[b] : (size_t)b * T_) * D + c;
-  float s = 0.f;
+  double s = 0.0;
   if (c < D)
-    for (int t = g; t < T; t += 4) s += p[(size_t)t * D];
+    for (int t = g; t < T; t += 4) s += (double)p[(size_t)t * D];
   part[g][threadIdx.x & 63] = s;
   __syncthreads();
-  const float mean = (part[0][threadIdx.x & 63] + part[1][threadIdx.x & 63] + part[2][threadIdx.x & 63] +
-                      part[3][threadIdx.x & 63]) / (float)T;
+  const double mean = (part[0][threadIdx.x & 63] + part[1][threadIdx.x & 63] + part[2][threadIdx.x & 63] +
+                       part[3][threadIdx.x & 63]) / (double)T;
   if (c < D)
-    for (int t = g; t < T; t += 4) p[(size_t)t * D] -= mean;
+    for (int t = g; t < T; t += 4) p[(size_t)t * D] = (float)((double)p[(size_t)t * D] - mean);
 }
 
 }  // namespace

@@ -22,6 +22,7 @@ constexpr int kPosK = 128, kPosGroups = 16, kPosGin = kHidden / kPosGroups, kPos
 constexpr int kConvK[7] = {10, 3, 3, 3, 3, 2, 2};
 constexpr int kConvS[7] = {5, 2, 2, 2, 2, 2, 2};
 constexpr int kDownsample = 320;
+constexpr int kMinSamples = 800;  // s3prl MIN_SECOND (0.05 s) * 16 kHz
 const char* const kPre = "frontend.upstream.upstream.model.";
 
 std::string hp(const std::string& n) { return std::string(kPre) + n; }
@@ -156,8 +157,13 @@ HubertPlan Model::Impl::hubert_plan(int B, const int* lens) const {
   std::vector<int> T[7], Tout(B);
   for (int k = 0; k < 7; ++k) T[k].resize(B);
   for (int b = 0; b < B; ++b) {
-    WSP_CHECK(lens[b] >= 400, "HuBERT needs at least 400 samples per utterance");
-    int t = lens[b];
+    WSP_CHECK(lens[b] >= 1, "HuBERT needs at least 1 sample per utterance");
+    // s3prl S3PRLUpstream.forward (MIN_SECOND = 0.05): an utterance shorter than
+    // 800 samples runs zero-padded to 800 (conv0 reads zeros past the real
+    // samples, and its GroupNorm statistics cover the padded frames); the
+    // output keeps len(range(0, W, 320)) frames of the real length W (the
+    // featurizer's length match trims the extra frame).
+    int t = std::max(lens[b], kMinSamples);
     for (int k = 0; k < 7; ++k) T[k][b] = t = (t - kConvK[k]) / kConvS[k] + 1;
     Tout[b] = (lens[b] + kDownsample - 1) / kDownsample;
   }
@@ -327,13 +333,13 @@ bool Model::is_frontend() const { return impl->hubert; }
 
 int Model::out_frames(int N) const {
   WSP_CHECK(impl->hubert, "out_frames: not a front-end handle");
-  WSP_CHECK(N >= 400, "HuBERT needs at least 400 samples");
+  WSP_CHECK(N >= 1, "HuBERT needs at least 1 sample");
   return (N + kDownsample - 1) / kDownsample;
 }
 
 size_t Model::frontend_workspace_bytes(int B, int N) const {
   WSP_CHECK(impl->hubert, "frontend_workspace_bytes: not a front-end handle");
-  WSP_CHECK(B > 0 && N >= 400, "HuBERT needs B >= 1 and N >= 400 samples");
+  WSP_CHECK(B > 0 && N >= 1, "HuBERT needs B >= 1 and N >= 1 samples");
   const std::vector<int> lens(B, N);
   return frontend_workspace_bytes_segments(B, lens.data());
 }
@@ -346,7 +352,7 @@ size_t Model::frontend_workspace_bytes_segments(int B, const int* lens) const {
 
 void Model::forward_frontend(const float* wav, int B, int N, float* feats, int cmn, void* ws, size_t ws_bytes,
                              hipStream_t s) {
-  WSP_CHECK(B > 0 && N >= 400, "HuBERT needs B >= 1 and N >= 400 samples");
+  WSP_CHECK(B > 0 && N >= 1, "HuBERT needs B >= 1 and N >= 1 samples");
   const std::vector<int> lens(B, N);
   forward_frontend_segments(wav, B, lens.data(), feats, nullptr, cmn, ws, ws_bytes, s);
 }

@@ -147,13 +147,14 @@ void launch_nhwc_to_tfc(const float* in, float* out, int B, int F, int T, int C,
 void launch_resnet_stem(const float* feats, int B, int T, int F, int C0, const float* w, const float* bias,
                         float* out, hipStream_t s);
 
-// Kaldi fbank + optional CMN.  `tables` = device copy of fbank_tables().
-constexpr int kFbankTableFloats = 1664 + 1024;
-void fbank_tables(float* host_tab);  // window, twiddles, sparse mel filters
+// Kaldi fbank (float64 arithmetic) + optional fused CMN.  `tables` = device
+// copy of fbank_tables().
+constexpr int kFbankTableDoubles = 1664 + 1024;
+void fbank_tables(double* host_tab);  // window, twiddles, sparse mel filters
 // Segmented: wseg / fseg = device int32 [B+1] sample / frame offsets, T = frames
 // of the longest utterance (grid size); N, ld unused.
 void launch_fbank(const void* wav, int dtype, int B, int N, int ld, float scale, float* feats,
-                  int T, int cmn, const float* tables, hipStream_t s, const int* wseg = nullptr,
+                  int T, int cmn, const double* tables, hipStream_t s, const int* wseg = nullptr,
                   const int* fseg = nullptr);
 
 // HuBERT-base front end (hubert.hip).

@@ -113,7 +113,7 @@ class S3prlFrontend(_HipHandle):
         return out
 
     def extract_segments(self, wavs, cmn: bool = False) -> Tuple[torch.Tensor, List[int]]:
-        """Ragged batch of whole utterances (sequence of 1-D [-1, 1] waveforms, >= 400
+        """Ragged batch of whole utterances (sequence of 1-D [-1, 1] waveforms, >= 1
         samples each) -> (feats [sum_b T_b][768] on the device, frame offsets [B+1]);
         rows of utterance b equal extract(wavs[b][None])[0]."""
         dev = torch.device("cuda", self._device if self._device is not None else torch.cuda.current_device())

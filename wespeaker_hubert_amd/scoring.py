@@ -38,8 +38,9 @@ def asnorm_stats(emb: torch.Tensor, cohort: torch.Tensor, top_n: int,
     c = l2_normalize(cohort, mean_vec)
     Ne, D = e.shape
     Nc = c.shape[0]
-    if not 1 <= top_n <= Nc:
-        raise ValueError(f"top_n={top_n} outside [1, {Nc}]")
+    if top_n < 1:
+        raise ValueError(f"top_n={top_n} must be >= 1")
+    top_n = min(int(top_n), Nc)  # score_norm.py:33 slices [:, :top_n]: an oversized top_n is the whole cohort
     nbytes = ctypes.c_size_t()
     _lib.check(_lib.load().wsp_asnorm_workspace_bytes(Ne, Nc, D, ctypes.byref(nbytes)), "asnorm ws")
     ws = torch.empty(nbytes.value, dtype=torch.uint8, device=e.device)
