@@ -155,6 +155,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--precision", type=int, default=1, help="1 = bf16x3 split MFMA, 0 = f32 MFMA")
     ap.add_argument("--x3-variant", type=int, default=None)
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra model option (wsp_model_set_option), e.g. res2_variant=1; repeatable")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing pass")
     ap.add_argument("--no-f32", action="store_true", help="skip the exact-f32 (precision 0) side measurement")
     ap.add_argument("--sustain-seconds", type=float, default=2.0,
@@ -337,6 +339,10 @@ def main():
         mm.set_option("precision", args.precision)
         if args.x3_variant is not None:
             mm.set_option("x3_variant", args.x3_variant)
+        if mm is model:
+            for kv in args.opt:
+                k, _, v = kv.partition("=")
+                mm.set_option(k, int(v))
         mm.to(dev)
 
     # inputs resident in HBM before the timed region (per-rank shard)
@@ -543,6 +549,7 @@ def main():
         "model_tflops": round(value * gf / 1e3, 2),
         "gflop_per_utt": round(gf, 3),
         "roofline": roof,
+        "options": args.opt or None,
         "kernels": kernels,
         "cpu_baseline": None,
     }

@@ -205,6 +205,11 @@ void Model::set_option(const std::string& key, int value) {
     for (const auto& p : impl->params) WSP_CHECK(!p.set, "option 'in_planes' must be set before the weights");
     impl->m_ch = value;
     impl->build_simam_params();
+  } else if (key == "res2_fused") {
+    WSP_CHECK(value == 0 || value == 1, "res2_fused must be 0 or 1");
+    impl->res2_fused = value;
+  } else if (key == "res2_variant") {
+    impl->res2_variant = value;
   } else if (key == "x3_variant") {
     WSP_CHECK(value >= 0 && value <= 6, "x3_variant must be 0..6");
     impl->x3_variant = value;

@@ -15,6 +15,7 @@
 
 #include "kernels.h"
 #include "model.h"
+#include "res2_chain.h"
 
 namespace wsp {
 
@@ -132,7 +133,12 @@ struct Model::Impl {
   struct Block {
     ConvW c1, c3, res2[7];
     LinW se1, se2;
+    // the 7 Res2Net convs packed for res2_chain.hip (one launch per block)
+    void* r2w = nullptr;
+    float *r2b = nullptr, *r2s = nullptr, *r2t = nullptr;
   } blk[3];
+  int res2_fused = 1;  // 0: the 7-launch GEMM chain (A/B option "res2_fused")
+  int res2_variant = 0;  // res2_chain.hip kernel variant (option "res2_variant")
   ConvW conv, pool1, pool2;
   LinW pool1_ctx;
   LinW head;
@@ -717,6 +723,42 @@ struct Model::Impl {
     }
   }
 
+  // Res2Net chain weights for res2_chain.hip: W_i [w][w][3] -> bf16 hi / lo in
+  // MFMA B-fragment order [7][3w/16][2][w/32][64 lanes][8], k = tap * w + c;
+  // conv bias and eval-BN affine per step [7][w].
+  void pack_res2(Block& b, const std::string& p, int w) {
+    const int KS = 3 * w / 16, NT = w / 32;
+    std::vector<uint16_t> pk((size_t)7 * KS * 2 * NT * 64 * 8);
+    std::vector<float> bias((size_t)7 * w), sc((size_t)7 * w), sh((size_t)7 * w);
+    for (int i = 0; i < 7; ++i) {
+      const std::string ci = p + ".1.convs." + std::to_string(i);
+      const auto& W = P(ci + ".weight");
+      const auto& bb = P(ci + ".bias");
+      std::vector<double> s, t;
+      bn_affine(p + ".1.bns." + std::to_string(i), s, t);
+      for (int n = 0; n < w; ++n) {
+        bias[(size_t)i * w + n] = bb[n];
+        sc[(size_t)i * w + n] = (float)s[n];
+        sh[(size_t)i * w + n] = (float)t[n];
+      }
+      for (int ks = 0; ks < KS; ++ks)
+        for (int jt = 0; jt < NT; ++jt)
+          for (int l = 0; l < 64; ++l)
+            for (int e = 0; e < 8; ++e) {
+              const int n = jt * 32 + (l & 31), k = ks * 16 + 8 * (l >> 5) + e;
+              const float v = W[((size_t)n * w + k % w) * 3 + k / w];
+              const uint16_t hi = f2bf(v), lo = f2bf(v - bf2f(hi));
+              const size_t o = ((((size_t)i * KS + ks) * 2) * NT + jt) * 64 + l;
+              pk[o * 8 + e] = hi;
+              pk[(o + (size_t)NT * 64) * 8 + e] = lo;
+            }
+    }
+    b.r2w = dev.upload_u16(pk);
+    b.r2b = dev.upload(bias);
+    b.r2s = dev.upload(sc);
+    b.r2t = dev.upload(sh);
+  }
+
   void finalize_ecapa() {
     const int w = C / 8;
     layer1 = pack_conv(P("layer1.conv.weight"), C, feat_dim, 5, P("layer1.conv.bias").data(), "layer1.bn");
@@ -729,6 +771,7 @@ struct Model::Impl {
         b.res2[i] = pack_conv(P(ci + ".weight"), w, w, 3, P(ci + ".bias").data(),
                               p + ".1.bns." + std::to_string(i));
       }
+      if (res2_chain_supported(w, li + 2)) pack_res2(b, p, w);
       b.c3 = pack_conv(P(p + ".2.conv.weight"), C, C, 1, P(p + ".2.conv.bias").data(), p + ".2.bn");
       b.se1 = pack_lin(P(p + ".3.linear1.weight").data(), 128, C, C, P(p + ".3.linear1.bias").data());
       b.se2 = pack_lin(P(p + ".3.linear2.weight").data(), C, 128, 128, P(p + ".3.linear2.bias").data());
@@ -885,7 +928,26 @@ struct Model::Impl {
       const int dil = li + 2;
       const float* xin = x[li + 1];
       gemm("conv1x1_CxC", b.c1, xin, C, h1, C, M, T, 1, 0, kActRelu, s, nullptr, true, 1);
-      for (int i = 0; i < 7; ++i) {
+      if (precision == 1 && res2_fused && b.r2w) {
+        // the whole chain in one launch (res2_chain.hip)
+        Res2Args r{};
+        r.x = h1;
+        r.out = h2;
+        r.ldx = r.ldo = C;
+        r.M = M;
+        r.T = T;
+        r.dil = dil;
+        r.rout = res2_chain_rout(dil, res2_variant);
+        r.seg = seg;
+        r.nseg = B;
+        r.w = b.r2w;
+        r.bias = b.r2b;
+        r.scale = b.r2s;
+        r.shift = b.r2t;
+        r.variant = res2_variant;
+        run("res2_k3", 7 * 2.0 * M * w * 3 * w, s, [&] { launch_res2_chain(r, w, s); });
+      }
+      for (int i = 0; i < 7 && !(precision == 1 && res2_fused && b.r2w); ++i) {
         ConvGemmArgs g{};
         if (i == 0) {
           g.amode = kACat;

@@ -1,0 +1,306 @@
+// Res2Net dilated-k3 chain of one SE_Res2Block in ONE launch (bf16x3 MFMA).
+//
+// Reference: Res2Conv1dReluBn.forward, ecapa_tdnn.py:64-78 —
+//   spx = split(x, w);  for i < 7: sp = spx[i] if i == 0 else sp + spx[i]
+//                                  sp = BN_i(ReLU(Conv1d_i(sp)))   (k3, dilation d, pad d)
+//   out = cat(sp_0 .. sp_6, spx[7])
+// The 7 convs form a serial chain whose every step reads the previous step's
+// output: run as 7 GEMM launches, each step round-trips HBM (read sp + spx[i],
+// write sp).  Here a block owns `rout` output rows and keeps the chain on chip:
+//   * a window of kR = 256 frame rows (the owned rows plus a 6d halo on each
+//     side) is the GEMM's M; step i is valid on window rows [i*d, kR - i*d)
+//     (the conv's +-d taps lose d rows per side per step), so after 7 steps the
+//     owned rows [6d, kR - 6d) are exact — halo recomputation instead of a
+//     cross-block exchange;
+//   * the conv input X_i = sp_{i-1} + spx[i] lives in LDS as bf16 hi / lo planes
+//     (x = hi + lo, the bf16x3 split of conv_gemm_x3.hip), rows XOR-swizzled by
+//     16-B chunk so the A-fragment ds_read_b128s are conflict-free; the k3 taps
+//     are row offsets into that image, and a tap that leaves its utterance reads
+//     a zero row (the reference's zero padding, per utterance of a ragged batch);
+//   * the step's epilogue (bias, ReLU, BN) stores the owned rows of sp_i to
+//     out[:, i*w ..] and writes X_{i+1} = sp_i + spx[i+1] (fp32 add, then split)
+//     back into the image;
+//   * W_i is host-packed in MFMA B-fragment order, so each wave reads its
+//     fragments straight from global memory (1 KB contiguous per instruction,
+//     L1/L2-resident, two k-steps ahead in registers): the X image is the only
+//     LDS operand, constant during a step, and the k-loop has no barrier;
+//   * R = 128-row windows (4 waves, 70 KB of LDS) run two blocks per CU, so one
+//     block's epilogue (addend loads, stores, image update) overlaps the other's
+//     MFMA loop; R = 256 (8 waves, 136 KB) halves the halo overhead instead.
+// HBM traffic per row: spx[0..6] read once (+ halo re-reads, mostly L2 hits of
+// the neighbouring block) and sp_0..6 written once.
+#include "gemm_common.h"
+#include "res2_chain.h"
+
+namespace wsp {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kPad = 4;  // image rows beyond each window edge (max dilation)
+
+template <int W, int R>
+struct Geo {
+  static constexpr int IR = R + 2 * kPad;          // image rows; row IR is the zero row
+  static constexpr int RB = 2 * W;                 // bytes per image row and plane
+  static constexpr int PLANE = (IR + 1) * RB;      // + the zero row
+  static constexpr int KS = 3 * W / 16;            // 16-deep MFMA k-steps per conv (K = 3W)
+  static constexpr int KC = W / 16;                // k-steps per tap
+  static constexpr int WST = 64 * W;               // one k-step of W: W cols x 16 k x (hi, lo) bf16
+  static constexpr int WN = 2, WM = R / 64, TM = 2, TN = W / 64;
+  static constexpr int NW = WM * WN;
+  static constexpr int NT = NW * 64;
+  static constexpr int LDS = 2 * PLANE;
+  // 16-B chunk swizzle: the 16 rows of a ds_read_b128 lane group land on 16
+  // distinct chunk slots of the 256-B bank row
+  __device__ __forceinline__ static int sw(int ir) { return W == 128 ? (ir & 15) : ((ir >> 1) & 7); }
+  __device__ __forceinline__ static int addr(int ir, int ch) {
+    return ir * RB + (((ch >> 3) ^ sw(ir)) << 4) + (ch & 7) * 2;
+  }
+};
+
+__device__ __forceinline__ unsigned short bf_bits(__bf16 x) { return __builtin_bit_cast(unsigned short, x); }
+
+template <int W, int R>
+__global__ __launch_bounds__(2 * R, R == 128 ? 2 : 1) void res2_chain_kernel(const Res2Args p) {
+  using G = Geo<W, R>;
+  constexpr int TM = G::TM, TN = G::TN, NT = G::NT, IR = G::IR;
+  static_assert(NT == 2 * R, "launch bounds assume 2R threads");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* xhi = smem;
+  unsigned char* xlo = smem + G::PLANE;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / G::WN;
+  const int wn = wave - wm * G::WN;
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+  const int d = p.dil;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring windows share an XCD L2 (halo rows)
+  const int own0 = blk * p.rout;
+  const int own1 = min(own0 + p.rout, p.M);
+  const int wr0 = own0 - 6 * d;  // window row 0
+
+  // ---- zero row + X_0 = spx[0] on image rows [0, IR) (window rows -kPad .. R + kPad)
+  if (tid < G::RB / 4) {
+    reinterpret_cast<unsigned*>(xhi + IR * G::RB)[tid] = 0u;
+    reinterpret_cast<unsigned*>(xlo + IR * G::RB)[tid] = 0u;
+  }
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x);
+  constexpr int C4 = W / 4;
+  for (int q = tid; q < IR * C4; q += NT) {
+    const int ir = q / C4;
+    const int c = (q - ir * C4) * 4;
+    const int m = wr0 + ir - kPad;
+    const f32x4 v = bload4(rx, (m >= 0 && m < p.M) ? (m * p.ldx + c) * 4 : kOOB);
+    bf16x4 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const __bf16 hh = (__bf16)v[e];
+      hi[e] = hh;
+      lo[e] = (__bf16)(v[e] - (float)hh);
+    }
+    const int a = G::addr(ir, c);
+    *reinterpret_cast<bf16x4*>(xhi + a) = hi;
+    *reinterpret_cast<bf16x4*>(xlo + a) = lo;
+  }
+
+  // ---- A-fragment rows: this lane's window row per tile, per tap (or the zero row)
+  int arow[TM][3], asw[TM][3];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = (wm * TM + i) * 32 + r32;
+    const int m = wr0 + r;
+    int t = -1, L = 0;
+    if (m >= 0 && m < p.M) {
+      if (p.seg) {
+        const int u = seg_of(p.seg, p.nseg, m);
+        t = m - p.seg[u];
+        L = p.seg[u + 1] - p.seg[u];
+      } else {
+        const int u = m / p.T;
+        t = m - u * p.T;
+        L = p.T;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int off = (j - 1) * d;
+      const bool ok = t >= 0 && t + off >= 0 && t + off < L;
+      const int ir = ok ? r + off + kPad : IR;
+      arow[i][j] = ir * G::RB;
+      asw[i][j] = G::sw(ir);
+    }
+  }
+
+  // ---- W fragments from global: k-step g, plane pl, column tile ct at
+  // ((g * 2 + pl) * (W / 32) + ct) * 1 KB + lane * 16
+  constexpr int kTotal = 7 * G::KS;
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w);
+  const int wlane = (wn * TN * 64 + lane) * 16;
+  auto wload = [&](int g, bf16x8 (&bh)[TN], bf16x8 (&bl)[TN]) {
+    const bool ok = g < kTotal;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int o = (g * 2 * (W / 32) + j) * 1024 + wlane;
+      bh[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? o : kOOB, 0, 0));
+      bl[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? o + (W / 32) * 1024 : kOOB, 0, 0));
+    }
+  };
+  bf16x8 wb0h[TN], wb0l[TN], wb1h[TN], wb1l[TN];
+  wload(0, wb0h, wb0l);
+  wload(1, wb1h, wb1l);
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(p.out);
+  f32x16 acc[TM][TN];
+  // one 16-deep k-step g (tap, channel block kc) on the W fragments in (bh, bl),
+  // which are then reloaded with k-step g + 2
+  auto kstep = [&](int g, int tap, int kc, bf16x8 (&bh)[TN], bf16x8 (&bl)[TN]) {
+    bf16x8 ah[TM], al[TM];
+    const int q = kc * 2 + h;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ar = tap == 0 ? arow[i][0] : tap == 1 ? arow[i][1] : arow[i][2];
+      const int as = tap == 0 ? asw[i][0] : tap == 1 ? asw[i][1] : asw[i][2];
+      const int a = ar + ((q ^ as) << 4);
+      ah[i] = *reinterpret_cast<const bf16x8*>(xhi + a);
+      al[i] = *reinterpret_cast<const bf16x8*>(xlo + a);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+    wload(g + 2, bh, bl);
+  };
+
+#pragma unroll 1
+  for (int step = 0; step < 7; ++step) {
+    const int gb = step * G::KS;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // KS is even: k-steps in pairs, W fragments alternating between two register sets
+#pragma unroll 1
+    for (int t = 0; t < G::KS - 2; t += 2) {
+      kstep(gb + t, t / G::KC, t % G::KC, wb0h, wb0l);
+      kstep(gb + t + 1, (t + 1) / G::KC, (t + 1) % G::KC, wb1h, wb1l);
+    }
+    // the next conv's addend spx[step + 1] (accumulator layout: row per register,
+    // col = lane & 31), issued two k-steps before the epilogue.  Row offsets are
+    // laundered per step (asm) so hipcc rebuilds them here instead of hoisting 64
+    // per-element addresses out of the step loop into registers.
+    int ldx4 = p.ldx * 4, ldo4 = p.ldo * 4, mw = wr0 + wm * TM * 32 + 4 * h;
+    asm volatile("" : "+s"(ldx4), "+s"(ldo4), "+v"(mw));
+    float nx[TM][TN][16];
+    if (step < 6) {
+      const __amdgpu_buffer_rsrc_t rxs = make_rsrc(p.x);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m0 = mw + i * 32;  // row of register 0
+        const int lo = -m0, hi = p.M - m0;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int base = (m0 * p.ldx + (step + 1) * W + (wn * TN + j) * 32 + r32) * 4;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rr = (r & 3) + 8 * (r >> 2);
+            nx[i][j][r] = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(rxs, (rr >= lo && rr < hi) ? base + rr * ldx4 : kOOB, 0, 0));
+          }
+        }
+      }
+    }
+    kstep(gb + G::KS - 2, 2, G::KC - 2, wb0h, wb0l);
+    kstep(gb + G::KS - 1, 2, G::KC - 1, wb1h, wb1l);
+    __syncthreads();  // every wave is done reading X_step
+
+    // ---- epilogue: sp = BN(ReLU(acc + b)); owned rows -> out; X_{step+1} -> LDS
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = (wn * TN + j) * 32 + r32;
+      const float bv = p.bias[step * W + col];
+      const float sc = p.scale[step * W + col];
+      const float sh = p.shift[step * W + col];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m0 = mw + i * 32;
+        const int olo = own0 - m0, ohi = own1 - m0;
+        const int base = (m0 * p.ldo + step * W + col) * 4;
+        const int irb = m0 - wr0 + kPad;  // image row of register 0
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rr = (r & 3) + 8 * (r >> 2);
+          const float y = fmaxf(acc[i][j][r] + bv, 0.f) * sc + sh;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rout,
+                                                (rr >= olo && rr < ohi) ? base + rr * ldo4 : kOOB, 0, 0);
+          if (step < 6) {
+            const float x = y + nx[i][j][r];
+            const __bf16 hh = (__bf16)x;
+            const __bf16 ll = (__bf16)(x - (float)hh);
+            // lanes l, l^1 hold channels col, col^1 of this row: the even lane
+            // writes both hi halves, the odd lane both lo halves (one 4-B store each)
+            const unsigned send = (lane & 1) ? bf_bits(hh) : bf_bits(ll);
+            const unsigned recv = (unsigned)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
+            const int a = G::addr(irb + rr, col & ~1);
+            if (lane & 1)
+              *reinterpret_cast<unsigned*>(xlo + a) = recv | ((unsigned)bf_bits(ll) << 16);
+            else
+              *reinterpret_cast<unsigned*>(xhi + a) = (unsigned)bf_bits(hh) | (recv << 16);
+          }
+        }
+      }
+    }
+    __syncthreads();  // X_{step+1} visible
+  }
+}
+
+}  // namespace
+
+bool res2_chain_supported(int w, int dil) { return (w == 64 || w == 128) && dil >= 1 && dil <= kPad; }
+
+static int res2_rows(int variant) { return (variant & 1) ? 256 : 128; }
+
+template <int W, int R>
+void launch_res2_k(const Res2Args& p, int nblk, hipStream_t s) {
+  hipLaunchKernelGGL((res2_chain_kernel<W, R>), dim3(nblk), dim3(Geo<W, R>::NT), (Geo<W, R>::LDS), s, p);
+}
+
+template <int W>
+void launch_res2_w(const Res2Args& p, int nblk, hipStream_t s) {
+  if (p.variant & 1)
+    launch_res2_k<W, 256>(p, nblk, s);
+  else
+    launch_res2_k<W, 128>(p, nblk, s);
+}
+
+void launch_res2_chain(const Res2Args& p, int w, hipStream_t s) {
+  WSP_CHECK(res2_chain_supported(w, p.dil), "res2_chain: width must be 64 or 128 and dilation 1..4");
+  WSP_CHECK(p.M > 0 && (p.seg || p.T > 0), "res2_chain: empty shape");
+  WSP_CHECK(p.rout == res2_chain_rout(p.dil, p.variant), "res2_chain: rout must be res2_chain_rout(dil, variant)");
+  WSP_CHECK((long long)p.M * p.ldx * 4 < (long long)kOOB && (long long)p.M * p.ldo * 4 < (long long)kOOB,
+            "res2_chain: operand exceeds 2 GiB (split the batch)");
+  WSP_CHECK(p.ldx >= 8 * w && p.ldo >= 7 * w && p.ldx % 4 == 0, "res2_chain: bad leading dimensions");
+  const int nblk = (p.M + p.rout - 1) / p.rout;
+  if (w == 128)
+    launch_res2_w<128>(p, nblk, s);
+  else
+    launch_res2_w<64>(p, nblk, s);
+  WSP_HIP(hipGetLastError());
+}
+
+int res2_chain_rout(int dil, int variant) { return res2_rows(variant) - 12 * dil; }
+
+}  // namespace wsp
