@@ -205,12 +205,12 @@ def simam_forward(feats: Tensor, sd: Dict[str, Tensor], arch: str) -> Tensor:
     return F.linear(asp(out, sd, "pooling.attention"), sd["bottleneck.weight"], sd["bottleneck.bias"])
 
 
-def forward(arch: str, feats: Tensor, sd: Dict[str, Tensor], emb_bn: bool = False):
+def forward(arch: str, feats: Tensor, sd: Dict[str, Tensor], emb_bn: bool = False, two_emb_layer: bool = False):
     """Registry dispatch — speaker_model.py:30-57 (prefix match).  Always (aux, embed)."""
     if arch.startswith("SimAM_ResNet"):
         return None, simam_forward(feats, sd, arch)
     if arch.startswith("ECAPA_TDNN"):
         return ecapa_forward(feats, sd, glob="GLOB" in arch, emb_bn=emb_bn)
     if arch.startswith("ResNet"):
-        return resnet_forward(feats, sd, arch)
+        return resnet_forward(feats, sd, arch, two_emb_layer)
     raise KeyError(arch)

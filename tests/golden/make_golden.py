@@ -76,6 +76,9 @@ MODEL_CASES = [
     ("ecapa_glob_c512_ssl768_b2_t250", "ECAPA_TDNN_GLOB_c512", dict(feat_dim=768, embed_dim=192), 16, 107, 2, 250, False),
     ("resnet34_b2_t200", "ResNet34", dict(feat_dim=80, embed_dim=256), 21, 201, 2, 200, True),
     ("resnet293_b1_t160", "ResNet293", dict(feat_dim=80, embed_dim=256), 22, 202, 1, 160, True),
+    # hub "english" backbone (cli/hub.py:88) and the two-embedding-layer head (resnet.py:158-161,196-201)
+    ("resnet221_b1_t120", "ResNet221", dict(feat_dim=80, embed_dim=256), 23, 203, 1, 120, True),
+    ("resnet34_2emb_b2_t150", "ResNet34", dict(feat_dim=80, embed_dim=256, two_emb_layer=True), 24, 204, 2, 150, True),
     # samresnet.py:124-166 (hub "vblinkp"/"vblinkf" backbone); ctor takes acoustic_dim
     ("simam34_b2_t200", "SimAM_ResNet34_ASP", dict(acoustic_dim=80, embed_dim=256), 31, 301, 2, 200, True),
     ("simam34_inpl32_b1_t97", "SimAM_ResNet34_ASP", dict(in_planes=32, acoustic_dim=40, embed_dim=128),
@@ -111,6 +114,7 @@ def make_models(out, only=None):
                    B=np.int64(B), T=np.int64(T), feat_dim=np.int64(feat_dim),
                    in_planes=np.int64(kw.get("in_planes", 64 if ctor.startswith("SimAM") else 32)),
                    embed_dim=np.int64(kw["embed_dim"]), emb_bn=np.int64(int(kw.get("emb_bn", False))),
+                   two_emb_layer=np.int64(int(kw.get("two_emb_layer", False))),
                    residual_tame=np.int64(int(tame)),
                    input_sum=np.float64(x.astype(np.float64).sum()), input_head=x.reshape(-1)[:16].copy(),
                    param_names=np.array([k for k in model.state_dict()]),

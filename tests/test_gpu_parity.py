@@ -89,7 +89,8 @@ def test_ecapa_matches_oracle_batched(arch, B, T, prec):
 def test_resnet_matches_reference_fixture(path):
     from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
     z = np.load(path, allow_pickle=False)
-    m = HipSpeakerModel(str(z["arch"]), feat_dim=int(z["feat_dim"]), embed_dim=int(z["embed_dim"]))
+    kw = dict(two_emb_layer=True) if "two_emb_layer" in z and int(z["two_emb_layer"]) else {}
+    m = HipSpeakerModel(str(z["arch"]), feat_dim=int(z["feat_dim"]), embed_dim=int(z["embed_dim"]), **kw)
     m.load_state_dict(synth_state_dict(int(z["weight_seed"]), m.state_dict_layout(), residual_tame=True))
     m.to(DEV)
     x = synth_feats(int(z["input_seed"]), int(z["B"]), int(z["T"]), int(z["feat_dim"]))

@@ -23,8 +23,9 @@ def load_case(path):
         spec = A.make_spec(arch, in_planes=int(z["in_planes"]), acoustic_dim=int(z["feat_dim"]),
                            embed_dim=int(z["embed_dim"]))
     else:
+        kw = dict(two_emb_layer=True) if "two_emb_layer" in z and int(z["two_emb_layer"]) else {}
         spec = A.make_spec(arch, feat_dim=int(z["feat_dim"]), embed_dim=int(z["embed_dim"]),
-                           emb_bn=bool(int(z["emb_bn"])))
+                           emb_bn=bool(int(z["emb_bn"])), **kw)
     plist = A.param_list(spec)
     sd = synth_state_dict(int(z["weight_seed"]), plist, residual_tame=bool(int(z["residual_tame"])))
     x = synth_feats(int(z["input_seed"]), int(z["B"]), int(z["T"]), int(z["feat_dim"]))
@@ -47,7 +48,8 @@ def test_oracle_matches_reference_forward(path):
     np.testing.assert_array_equal(x.reshape(-1)[:16], z["input_head"])
     sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
     with torch.no_grad():
-        _, emb = models_ref.forward(spec.arch, torch.from_numpy(x), sdt, emb_bn=spec.emb_bn)
+        _, emb = models_ref.forward(spec.arch, torch.from_numpy(x), sdt, emb_bn=spec.emb_bn,
+                                    two_emb_layer=spec.two_emb_layer)
     ref = z["embed"]
     assert emb.shape == ref.shape
     np.testing.assert_allclose(emb.numpy(), ref, atol=2e-5, rtol=0)

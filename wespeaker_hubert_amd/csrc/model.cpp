@@ -55,7 +55,6 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
         {"ResNet293", {true, {10, 20, 64, 3}}}};
     auto it = kRes.find(arch);
     WSP_CHECK(it != kRes.end(), "unsupported arch " + arch);
-    WSP_CHECK(!two_emb, "ResNet two_emb_layer=True is not implemented");
     WSP_CHECK(feat_dim >= 8, "ResNet feat_dim must be >= 8");
     m.ecapa = false;
     m.x3_variant = 3;  // HBM-bound 1x1 convs: two 128 x 128 blocks per CU (+4 % over variant 4)

@@ -155,7 +155,7 @@ struct Model::Impl {
     int stride = 1, in_planes = 0, planes = 0, out_planes = 0;
   };
   std::vector<RBlock> rblocks;
-  LinW seg1;
+  LinW seg1, seg2;  // seg2: two_emb_layer's seg_2 with the affine-free seg_bn_1 folded in
 
   // SimAM-ResNet (samresnet.py:20-166): basic blocks whose bn2 output passes
   // SimAM before the shortcut add, ASP pooling, `bottleneck` Linear.
@@ -360,6 +360,13 @@ struct Model::Impl {
     const int stats_dim = (feat_dim / 8) * m_ch * 8 * exp;
     add("seg_1.weight", {embed_dim, stats_dim * 2});
     add("seg_1.bias", {embed_dim});
+    if (two_emb) {  // resnet.py:158-161: BatchNorm1d(affine=False) + seg_2
+      add("seg_bn_1.running_mean", {embed_dim});
+      add("seg_bn_1.running_var", {embed_dim});
+      add("seg_bn_1.num_batches_tracked", {});
+      add("seg_2.weight", {embed_dim, embed_dim});
+      add("seg_2.bias", {embed_dim});
+    }
   }
 
   // conv -> BN (eval) folded into the weights: W' = W * s[n], bias = shift.
@@ -413,6 +420,26 @@ struct Model::Impl {
           for (int c = 0; c < C4; ++c)
             wp[(size_t)n * K + f * 2 * C4 + sidx * C4 + c] = W[(size_t)n * K + sidx * C4 * F4 + c * F4 + f];
     seg1 = pack_lin(wp.data(), embed_dim, K, K, P("seg_1.bias").data());
+    if (two_emb) {
+      // embed_b = seg_2(BN(relu(embed_a))), BN without affine (resnet.py:196-200):
+      // W2 ((r - rm) / sqrt(rv + eps)) + b2 = (W2 diag(s)) r + (b2 - W2 (rm s))
+      const auto& rm = P("seg_bn_1.running_mean");
+      const auto& rv = P("seg_bn_1.running_var");
+      const auto& W2 = P("seg_2.weight");
+      const auto& b2 = P("seg_2.bias");
+      const int D = embed_dim;
+      std::vector<float> w2((size_t)D * D), bb(D);
+      for (int n = 0; n < D; ++n) {
+        double acc = b2[n];
+        for (int k = 0; k < D; ++k) {
+          const double sk = 1.0 / std::sqrt((double)rv[k] + kBnEps);
+          w2[(size_t)n * D + k] = (float)(W2[(size_t)n * D + k] * sk);
+          acc -= (double)W2[(size_t)n * D + k] * rm[k] * sk;
+        }
+        bb[n] = (float)acc;
+      }
+      seg2 = pack_lin(w2.data(), D, D, D, bb.data());
+    }
   }
 
   struct RShapes {
@@ -547,9 +574,16 @@ struct Model::Impl {
       // TSTP over frames for every (utterance, freq) row block, then seg_1
       run("tstp_head", 0, s, [&] {
         launch_frame_stats(x, Ci, nb * Fi, Ti, Ci, pooled, 2 * Ci, 1, Ci, s);
-        launch_small_linear({pooled, Fi * 2 * Ci, seg1.wt, seg1.bias, embed + (size_t)b0 * embed_dim, embed_dim, nb,
-                             Fi * 2 * Ci, embed_dim, 0},
-                            s);
+        float* e_out = embed + (size_t)b0 * embed_dim;
+        if (two_emb) {
+          // relu(seg_1(stats)) into the free conv1 buffer, then the folded seg_bn_1 + seg_2
+          launch_small_linear({pooled, Fi * 2 * Ci, seg1.wt, seg1.bias, Y1, embed_dim, nb, Fi * 2 * Ci, embed_dim, 1},
+                              s);
+          launch_small_linear({Y1, embed_dim, seg2.wt, seg2.bias, e_out, embed_dim, nb, embed_dim, embed_dim, 0}, s);
+        } else {
+          launch_small_linear({pooled, Fi * 2 * Ci, seg1.wt, seg1.bias, e_out, embed_dim, nb, Fi * 2 * Ci, embed_dim, 0},
+                              s);
+        }
       });
     }
   }

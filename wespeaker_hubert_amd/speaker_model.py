@@ -180,8 +180,6 @@ class HipSpeakerModel(_HipHandle):
     def __init__(self, arch: str, **model_args):
         super().__init__()
         self.spec: ModelSpec = make_spec(arch, **model_args)
-        if self.spec.two_emb_layer:
-            raise NotImplementedError("two_emb_layer=True is not implemented on the HIP path")
         self._layout = param_list(self.spec)
         if self.spec.family == "simam" and self.spec.m_channels != 64:
             self._options["in_planes"] = self.spec.m_channels  # before the weights (samresnet.py:124)
