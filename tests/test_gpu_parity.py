@@ -55,8 +55,9 @@ def _hip_model(arch, seed, precision=1, variant=5, **kw):
     return m.to(DEV), sd
 
 
-PREC = [(1, 5), (1, 4), (1, 3), (1, 2), (1, 1), (1, 0), (0, 0)]
-PREC_IDS = ["bf16x3_256sq", "bf16x3_256swz", "bf16x3_128swz", "bf16x3_dma", "bf16x3_256", "bf16x3_128", "f32"]
+PREC = [(1, 5), (1, 4), (1, 3), (1, 2), (1, 9), (1, 1), (1, 0), (0, 0)]
+PREC_IDS = ["bf16x3_256sq", "bf16x3_256swz", "bf16x3_128swz", "bf16x3_dma", "bf16x3_dma256", "bf16x3_256", "bf16x3_128",
+            "f32"]
 
 
 @pytest.mark.parametrize("prec", PREC, ids=PREC_IDS)

@@ -15,6 +15,7 @@
 //   * out-of-range buffer offsets (conv padding, tail tiles) load zeros.
 // Block 256 x 128 x 32, 8 waves (4 x 2), each 2 x 2 tiles of 32x32x16 MFMA.
 #include "gemm_common.h"
+#include "gemm_dma.h"
 
 namespace wsp {
 
@@ -24,7 +25,17 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int BK = 32;
-constexpr int NST = 3;
+
+// s_waitcnt vmcnt(N) needs a literal
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned char* lds, int voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, 0, 0, 0);
@@ -42,13 +53,15 @@ __device__ __forceinline__ void split8(const f32x4& x0, const f32x4& x1, bf16x8&
   }
 }
 
-template <int TM, int TN, bool UNI, int ROLE>
-__global__ __launch_bounds__(512, 2) void conv_gemm_x3d(const ConvGemmArgs p,
-                                                        const __bf16* __restrict__ whi,
-                                                        const __bf16* __restrict__ wlo) {
-  constexpr int WM = 4, WN = 2, NW = 8;
-  constexpr int BM = WM * TM * 32;       // 256
-  constexpr int BN = WN * TN * 32;       // 128
+// WM x WN waves of TM x TN 32x32 tiles, NST-stage LDS ring (NST - 1 tiles in
+// flight behind the one being multiplied).
+template <int WM, int WN, int TM, int TN, int NST, bool UNI, int ROLE>
+__global__ __launch_bounds__(WM* WN * 64, WM* WN / 4) void conv_gemm_x3d(const ConvGemmArgs p,
+                                                                          const __bf16* __restrict__ whi,
+                                                                          const __bf16* __restrict__ wlo) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
   constexpr int A_BYTES = BM * BK * 4;   // fp32 rows of 128 B
   constexpr int B_IMG = BN * BK * 2;     // bf16 rows of 64 B
   constexpr int STAGE = A_BYTES + 2 * B_IMG;
@@ -179,19 +192,17 @@ __global__ __launch_bounds__(512, 2) void conv_gemm_x3d(const ConvGemmArgs p,
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nk = p.Kp / BK;
-  issue(0, 0, true);
-  issue(BK, 1, nk > 1);
+#pragma unroll
+  for (int s0 = 0; s0 < NST - 1; ++s0) issue(s0 * BK, s0, s0 < nk);
 
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt landed (this wave's part); the barrier publishes every wave's
     // part and retires all reads of the stage the next issue overwrites.
-    if constexpr (OPS == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if constexpr (OPS == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_vmcnt<OPS * (NST - 2)>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    issue((kt + 2) * BK, (kt + 2) % NST, kt + 2 < nk);
+    issue((kt + NST - 1) * BK, (kt + NST - 1) % NST, kt + NST - 1 < nk);
     const unsigned char* st = smem + (kt % NST) * STAGE;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -217,20 +228,31 @@ __global__ __launch_bounds__(512, 2) void conv_gemm_x3d(const ConvGemmArgs p,
         }
     }
   }
-  // drain the (dummy) DMA still in flight before the workgroup's LDS is released
+  // drain the (dummy) DMA still in flight before the LDS is reused / released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // the fused column sums reuse the LDS
 
-  gemm_epilogue<TM, TN>(p, acc, m0, n0, wm, wn, lane);
+  gemm_epilogue<TM, TN, WM, WN>(p, acc, m0, n0, wm, wn, lane, smem);
 }
 
-template <bool UNI, int ROLE>
+template <int WM, int WN, int TM, int TN, int NST, bool UNI, int ROLE>
 void launch_d(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
-  constexpr int BM = 256, BN = 128;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int STAGE = BM * BK * 4 + 2 * BN * BK * 2;
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
-  hipLaunchKernelGGL((conv_gemm_x3d<2, 2, UNI, ROLE>), dim3(nwg), dim3(512), (size_t)NST * STAGE, s, p,
-                     whi, wlo);
+  hipLaunchKernelGGL((conv_gemm_x3d<WM, WN, TM, TN, NST, UNI, ROLE>), dim3(nwg), dim3(WM * WN * 64),
+                     (size_t)NST * STAGE, s, p, whi, wlo);
   WSP_HIP(hipGetLastError());
+}
+
+template <int WM, int WN, int TM, int TN, int NST>
+void launch_dv(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s) {
+  if (!uniform_ktiles(p))
+    launch_d<WM, WN, TM, TN, NST, false, 0>(p, h, l, s);
+  else if (p.role == 1)
+    launch_d<WM, WN, TM, TN, NST, true, 1>(p, h, l, s);
+  else
+    launch_d<WM, WN, TM, TN, NST, true, 0>(p, h, l, s);
 }
 
 }  // namespace
@@ -240,19 +262,28 @@ bool conv_gemm_dma_supported(const ConvGemmArgs& p) {
          p.stride <= 1 && (p.Ti == 0 || p.Ti == p.T) && !p.gcols && !p.seg;
 }
 
-void launch_conv_gemm_dma(const ConvGemmArgs& args, const void* whi, const void* wlo, hipStream_t s) {
+bool conv_gemm_dma_v_supported(const ConvGemmArgs& p, int variant) {
+  if (variant == 0) return conv_gemm_dma_supported(p);
+  return !p.conv2d && p.amode == kACat && p.N % 256 == 0 && (uniform_ktiles(p) || p.cseg[1] == p.cin) &&
+         p.stride <= 1 && (p.Ti == 0 || p.Ti == p.T) && !p.gcols && !p.seg;
+}
+
+void launch_conv_gemm_dma_v(const ConvGemmArgs& args, const void* whi, const void* wlo, int variant, hipStream_t s) {
   const ConvGemmArgs p = normalized(args);
   check_conv_args(p, "conv_gemm_dma");
-  WSP_CHECK(!p.colsum, "conv_gemm_dma: column sums are a bf16x3-kernel epilogue");
-  WSP_CHECK(conv_gemm_dma_supported(p), "conv_gemm_dma: unsupported operand layout");
+  WSP_CHECK(conv_gemm_dma_v_supported(p, variant), "conv_gemm_dma: unsupported operand layout");
+  if (p.colsum) WSP_CHECK(!p.row_bias && p.T >= 256, "conv_gemm_dma: column sums need T >= 256 and no row bias");
   const __bf16* h = static_cast<const __bf16*>(whi);
   const __bf16* l = static_cast<const __bf16*>(wlo);
-  if (!uniform_ktiles(p))
-    launch_d<false, 0>(p, h, l, s);
-  else if (p.role == 1)
-    launch_d<true, 1>(p, h, l, s);
-  else
-    launch_d<true, 0>(p, h, l, s);
+  switch (variant) {
+    case 0: launch_dv<4, 2, 2, 2, 3>(p, h, l, s); break;   // 256 x 128, 8 waves, 3 stages
+    case 2: launch_dv<4, 2, 2, 4, 2>(p, h, l, s); break;   // 256 x 256, 8 waves of 64 x 128, 2 stages
+    default: throw InvalidArg{"conv_gemm_dma: unknown variant"};
+  }
+}
+
+void launch_conv_gemm_dma(const ConvGemmArgs& args, const void* whi, const void* wlo, hipStream_t s) {
+  launch_conv_gemm_dma_v(args, whi, wlo, 0, s);
 }
 
 }  // namespace wsp

@@ -207,10 +207,13 @@ void Model::set_option(const std::string& key, int value) {
   } else if (key == "res2_fused") {
     WSP_CHECK(value == 0 || value == 1, "res2_fused must be 0 or 1");
     impl->res2_fused = value;
+  } else if (key == "astp_fused") {
+    WSP_CHECK(value == 0 || value == 1, "astp_fused must be 0 or 1");
+    impl->astp_fused_on = value;
   } else if (key == "res2_variant") {
     impl->res2_variant = value;
   } else if (key == "x3_variant") {
-    WSP_CHECK(value >= 0 && value <= 6, "x3_variant must be 0..6");
+    WSP_CHECK((value >= 0 && value <= 6) || value == 9, "x3_variant must be 0..6 or 9");
     impl->x3_variant = value;
   } else {
     throw InvalidArg{"unknown option " + key};

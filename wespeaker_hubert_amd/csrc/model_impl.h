@@ -16,6 +16,8 @@
 #include "kernels.h"
 #include "model.h"
 #include "res2_chain.h"
+#include "gemm_dma.h"
+#include "astp_fused.h"
 
 namespace wsp {
 
@@ -140,6 +142,8 @@ struct Model::Impl {
   int res2_fused = 1;  // 0: the 7-launch GEMM chain (A/B option "res2_fused")
   int res2_variant = 0;  // res2_chain.hip kernel variant (option "res2_variant")
   ConvW conv, pool1, pool2;
+  void* pool2_frag = nullptr;  // pool.linear2 in MFMA B-fragment order for astp_fused.hip
+  int astp_fused_on = 1;       // 0: linear2 GEMM + separate pooling kernel (option "astp_fused")
   LinW pool1_ctx;
   LinW head;
 
@@ -195,6 +199,8 @@ struct Model::Impl {
   // 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA
   int precision = 1;
   int x3_variant = 5;  // 256 x 256 bf16x3 tiles where N % 256 == 0, else 256 x 128 (tools/gemm_bench)
+  // conv_gemm_x3 variant behind x3_variant (the DMA selections 2 / 9 fall back to 5)
+  int x3_base() const { return (x3_variant == 2 || x3_variant >= 7) ? 5 : x3_variant; }
 
   // profiling
   bool prof = false;
@@ -270,6 +276,25 @@ struct Model::Impl {
       cw.shift = dev.upload(t);
     }
     return cw;
+  }
+
+  // Linear / 1x1-conv weight [N][K] -> bf16 hi / lo in MFMA B-fragment order
+  // [K/16 k-steps][2 planes][N/32 column tiles][64 lanes][8]: lane l of a
+  // 32x32x16 MFMA holds W[n = 32 j + (l & 31)][k = 16 ks + 8 (l >> 5) + e].
+  void* pack_frag(const std::vector<float>& w, int N, int K) {
+    const int KS = K / 16, NT = N / 32;
+    std::vector<uint16_t> pk((size_t)KS * 2 * NT * 64 * 8);
+    for (int ks = 0; ks < KS; ++ks)
+      for (int jt = 0; jt < NT; ++jt)
+        for (int l = 0; l < 64; ++l)
+          for (int e = 0; e < 8; ++e) {
+            const float v = w[(size_t)(jt * 32 + (l & 31)) * K + ks * 16 + 8 * (l >> 5) + e];
+            const uint16_t hi = f2bf(v), lo = f2bf(v - bf2f(hi));
+            const size_t o = (((size_t)ks * 2 * NT + jt) * 64 + l) * 8 + e;
+            pk[o] = hi;
+            pk[o + (size_t)NT * 64 * 8] = lo;
+          }
+    return dev.upload_u16(pk);
   }
 
   // Linear weight [N][K] (row-major, ldk) -> k-major [K][N]
@@ -507,7 +532,7 @@ struct Model::Impl {
     g.kw = kw;
     g.res = res;
     g.ldres = ldres;
-    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 5 : x3_variant, s); });
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_base(), s); });
   }
   void gemm1x1(const char* tag, const ConvW& cw, const float* a0, float* out, int M, int act, const float* res,
                hipStream_t s) {
@@ -519,7 +544,7 @@ struct Model::Impl {
     fill(g, cw, M, M, 1, 0, out, cw.N, act, nullptr, true);
     g.res = res;
     g.ldres = cw.N;
-    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 5 : x3_variant, s); });
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_base(), s); });
   }
 
   void forward_resnet(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
@@ -825,6 +850,7 @@ struct Model::Impl {
       }
     }
     pool2 = pack_conv(P("pool.linear2.weight"), 1536, 128, 1, P("pool.linear2.bias").data(), "");
+    pool2_frag = pack_frag(P("pool.linear2.weight"), 1536, 128);
     // head: y = Linear(BN(p)) [-> bn2] folded to y = W' p + b'
     {
       std::vector<double> s, t;
@@ -882,10 +908,13 @@ struct Model::Impl {
     run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch(g, cw, s); });
   }
   void launch(const ConvGemmArgs& g, const ConvW& cw, hipStream_t s) {
-    if (precision == 1 && x3_variant == 2 && conv_gemm_dma_supported(g))
-      launch_conv_gemm_dma(g, cw.whi, cw.wlo, s);
+    // x3_variant 2 / 9: LDS-DMA staged kernels (conv_gemm_dma.hip variants 0 / 2) where
+    // their operand layouts allow, else the register-staged variant 5
+    const int dv = x3_variant == 2 ? 0 : x3_variant == 9 ? 2 : -1;
+    if (precision == 1 && dv >= 0 && conv_gemm_dma_v_supported(g, dv))
+      launch_conv_gemm_dma_v(g, cw.whi, cw.wlo, dv, s);
     else if (precision == 1)
-      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant == 2 ? 5 : x3_variant, s);
+      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_base(), s);
     else
       launch_conv_gemm(g, s);
   }
@@ -953,7 +982,7 @@ struct Model::Impl {
     double* sesum = reinterpret_cast<double*>(ws + off[16]);
     // SE squeeze fused into conv3's epilogue (per-utterance f64 column sums) on the
     // bf16x3 path for uniform batches whose utterances span >= one block of rows
-    const int se_bm = precision == 1 ? conv_gemm_x3_block_rows(ConvGemmArgs{.N = C}, x3_variant == 2 ? 5 : x3_variant) : 0;
+    const int se_bm = precision == 1 ? conv_gemm_x3_block_rows(ConvGemmArgs{.N = C}, x3_base()) : 0;
     const bool se_fused = precision == 1 && !seg && T >= se_bm;
 
     gemm("layer1", layer1, feats, feat_dim, x[1], C, M, T, 1, 2, kActRelu, s);
@@ -1045,8 +1074,14 @@ struct Model::Impl {
     } else {
       gemm("pool_linear1", pool1, xp, 1536, att, 128, M, T, 1, 0, kActTanh, s);
     }
-    gemm("pool_linear2", pool2, att, 128, logit, 1536, M, T, 1, 0, kActNone, s);
-    run("astp", 0, s, [&] { launch_astp_pool(logit, xp, B, T, 1536, pooled, s, seg); });
+    if (precision == 1 && astp_fused_on) {
+      // linear2 + softmax over frames + attentive mean / std in one pass (astp_fused.hip)
+      AstpArgs a{att, xp, 1536, B, T, 1536, seg, pool2_frag, pool2.bias, 1e-7f, pooled};
+      run("astp", 2.0 * M * 1536 * 128, s, [&] { launch_astp_fused(a, s); });
+    } else {
+      gemm("pool_linear2", pool2, att, 128, logit, 1536, M, T, 1, 0, kActNone, s);
+      run("astp", 0, s, [&] { launch_astp_pool(logit, xp, B, T, 1536, pooled, s, seg); });
+    }
     run("head", 0, s, [&] {
       launch_small_linear({pooled, 3072, head.wt, head.bias, embed, embed_dim, B, 3072, embed_dim, 0}, s);
     });
