@@ -339,10 +339,9 @@ def main():
         mm.set_option("precision", args.precision)
         if args.x3_variant is not None:
             mm.set_option("x3_variant", args.x3_variant)
-        if mm is model:
-            for kv in args.opt:
-                k, _, v = kv.partition("=")
-                mm.set_option(k, int(v))
+        for kv in args.opt:
+            k, _, v = kv.partition("=")
+            mm.set_option(k, int(v))
         mm.to(dev)
 
     # inputs resident in HBM before the timed region (per-rank shard)

@@ -15,7 +15,7 @@ rc=$?; echo "trace rc=$rc"; tail -n 3 $OUT/trace.log; ok $rc || exit $rc
 i=0
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32 GRBM_GUI_ACTIVE" "TCC_HIT_sum TCC_MISS_sum" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 600 rocprofv3 --pmc $pmc --output-format csv -d $OUT/pmc$i -o p -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile $EXTRA > $OUT/pmc$i.log 2>&1
+  timeout -k 10 600 rocprofv3 --pmc $pmc --output-format csv -d $OUT/pmc$i -o p -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-f32 --sustain-seconds 0 $EXTRA > $OUT/pmc$i.log 2>&1
   rc=$?; echo "pmc$i ($pmc) rc=$rc"; tail -n 2 $OUT/pmc$i.log; ok $rc || exit $rc
 done
 exit 0

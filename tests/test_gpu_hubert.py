@@ -161,3 +161,30 @@ def test_ragged_batch_equals_batch_of_one(sd_np, sd_t, layer, multi):
                     ref = hubert_ref.s3prl_upstream(torch.from_numpy(w[None]), sd_t)[layer]
             ref = _cmn(ref)[0]
             assert (got.cpu() - ref).abs().max().item() <= FEAT_ATOL
+
+
+@pytest.mark.parametrize("W", [16000, 100000])
+def test_lds_attention_matches_streaming_kernel_and_oracle(sd_np, sd_t, W):
+    """attn.hip (K / V staged once per 256-key block in LDS) against the streaming
+    mha_kernel (option attn_lds=0) and the oracle; W = 100000 gives 312 frames:
+    two query blocks and two key blocks per (utterance, head)."""
+    wav = _wav(17, 2, W)
+    fe = _frontend(sd_np)
+    got = fe.extract(torch.from_numpy(wav).to(DEV)).cpu()
+    fe0 = _frontend(sd_np)
+    fe0.set_option("attn_lds", 0)
+    old = fe0.extract(torch.from_numpy(wav).to(DEV)).cpu()
+    assert float((got - old).abs().max()) < 2e-5
+    with torch.no_grad():
+        ref = hubert_ref.s3prl_frontend(torch.from_numpy(wav), sd_t)
+    assert float((got - ref).abs().max()) < FEAT_ATOL
+
+
+def test_lds_attention_ragged_long_utterances(sd_np):
+    fe = _frontend(sd_np)
+    lens = [100000, 3200, 90000, 16000]
+    wavs = [_wav(60 + i, 1, n)[0] for i, n in enumerate(lens)]
+    feats, offs = fe.extract_segments([torch.from_numpy(w) for w in wavs], cmn=True)
+    for i, w in enumerate(wavs):
+        one = fe.extract(torch.from_numpy(w[None]).to(DEV), cmn=True)[0]
+        np.testing.assert_allclose(feats[offs[i]:offs[i + 1]].cpu().numpy(), one.cpu().numpy(), atol=1e-5, rtol=0)

@@ -1,0 +1,13 @@
+// HuBERT self-attention with K / V staged once per key block in LDS (attn.hip).
+#pragma once
+
+#include "common.h"
+
+namespace wsp {
+
+// softmax(Q K^T / sqrt(dh)) V per (utterance, head); qkv [rows][ldq] = [q | k | v]
+// (H*dh each), out [rows][ldo].  Same contract as launch_mha (kernels.h).
+void launch_attn(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s,
+                 const int* seg = nullptr);
+
+}  // namespace wsp

@@ -1,0 +1,221 @@
+// HuBERT self-attention, softmax(Q K^T / 8) V per (utterance, head), on bf16x3
+// MFMA with K and V resident in LDS (fairseq MultiheadAttention as used by the
+// s3prl hubert upstream; restated in oracle/hubert_ref.py).
+//
+// A block owns 256 queries (8 waves x 32) of one (utterance, head) and walks
+// the keys in blocks of 256: each key block is staged ONCE into LDS already
+// split into bf16 hi / lo planes — K as [key][64 d] (128-B rows, 16-B chunks
+// XOR-swizzled by (key >> 1) & 7: conflict-free A-fragment reads) and V^T as
+// [64 d][keys] (520-B rows: conflict-free 8-B reads) — so the per-chunk loop
+// has no global loads, no VALU split of K / V and no barrier.  Per 32-key chunk
+// each wave computes S^T = K_c Q^T (queries on the lanes), an online softmax per
+// lane column, then O^T += V_c^T P with P taken from the S^T accumulators
+// (k order 16 s + 8 (j >> 2) + 4 h + (j & 3), cdna_hip_programming.md §3).
+// For 5 s utterances (249 frames) one block per (utterance, head) stages the
+// whole K / V once; the previous kernel (hubert.hip mha_kernel) streamed 32-key
+// chunks through a register / LDS ring with a barrier and an exposed global
+// load per chunk.
+#include "attn.h"
+#include "gemm_common.h"
+
+#include <cfloat>
+
+namespace wsp {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kDh = 64;                 // head dim
+constexpr int kKB = 256;                // keys per staged block
+constexpr int kQB = 256;                // queries per workgroup (8 waves x 32)
+constexpr int kVRow = 520;              // V^T row stride in bytes (260 bf16: 2-dword bank shift per row)
+constexpr int kKPlane = kKB * kDh * 2;  // 32 KB per K plane
+constexpr int kVPlane = kDh * kVRow;    // 33 KB per V^T plane
+constexpr int kLds = 2 * kKPlane + 2 * kVPlane;
+
+__device__ __forceinline__ int k_addr(int key, int chunk) {  // byte offset of a 16-B chunk of K row `key`
+  return key * 128 + ((chunk ^ ((key >> 1) & 7)) << 4);
+}
+
+__device__ __forceinline__ void split8(const f32x4 a, const f32x4 b, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 h0 = (__bf16)a[e], h1 = (__bf16)b[e];
+    hi[e] = h0;
+    hi[e + 4] = h1;
+    lo[e] = (__bf16)(a[e] - (float)h0);
+    lo[e + 4] = (__bf16)(b[e] - (float)h1);
+  }
+}
+
+__device__ __forceinline__ f32x16 mma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
+                                       f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(512, 2) void attn_kernel(const float* __restrict__ qkv, int ldq, float* __restrict__ out,
+                                                      int ldo, int T_, int D, float scale, const int* __restrict__ seg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* kh_s = smem;
+  unsigned char* kl_s = smem + kKPlane;
+  unsigned char* vh_s = smem + 2 * kKPlane;
+  unsigned char* vl_s = vh_s + kVPlane;
+
+  const int b = blockIdx.z, head = blockIdx.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const size_t rbase = seg ? (size_t)seg[b] : (size_t)b * T_;
+  const int T = seg ? seg[b + 1] - seg[b] : T_;
+  const int q0 = blockIdx.x * kQB;
+  if (q0 >= T) return;  // block-uniform (segmented: grid sized by the longest utterance)
+  const float* base = qkv + rbase * ldq;
+  const int q = q0 + wave * 32 + r;
+  const bool wave_live = q0 + wave * 32 < T;  // wave-uniform
+
+  // Q^T fragments (B operand of S^T = K Q^T): lane = query r, d = 16 s + 8 hh + e;
+  // pre-scaled by 1/sqrt(dh) = 1/8 (exact in binary)
+  bf16x8 qh[4], ql[4];
+  {
+    const float* qr = base + (size_t)min(q, T - 1) * ldq + head * kDh + 8 * hh;
+    const float sc = q < T ? scale : 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      split8(*reinterpret_cast<const f32x4*>(qr + 16 * s) * sc, *reinterpret_cast<const f32x4*>(qr + 16 * s + 4) * sc,
+             qh[s], ql[s]);
+  }
+
+  f32x16 o[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[t][e] = 0.f;
+  float m = -FLT_MAX, l = 0.f;
+
+  for (int k0 = 0; k0 < T; k0 += kKB) {
+    const int nk = min(kKB, T - k0);
+    if (k0 > 0) __syncthreads();  // the previous key block is no longer read
+    // ---- stage keys [k0, k0 + 256): K and V rows as hi / lo bf16 (zeros past T); all
+    // 16 loads of a thread are issued before the first conversion
+    constexpr int kPer = kKB * (kDh / 4) / 512;  // float4 pieces of K (and of V) per thread
+    f32x4 kv[kPer], vv[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int f = tid + 512 * i, key = f >> 4, d4 = (f & 15) * 4;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const float* row = base + (size_t)(k0 + min(key, nk - 1)) * ldq + head * kDh + d4;
+      kv[i] = key < nk ? *reinterpret_cast<const f32x4*>(row + D) : z;
+      vv[i] = key < nk ? *reinterpret_cast<const f32x4*>(row + 2 * D) : z;
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int f = tid + 512 * i, key = f >> 4, d4 = (f & 15) * 4;
+      bf16x4 h4, l4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const __bf16 h0 = (__bf16)kv[i][e];
+        h4[e] = h0;
+        l4[e] = (__bf16)(kv[i][e] - (float)h0);
+      }
+      const int ka = k_addr(key, d4 >> 3) + (d4 & 7) * 2;
+      *reinterpret_cast<bf16x4*>(kh_s + ka) = h4;
+      *reinterpret_cast<bf16x4*>(kl_s + ka) = l4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const __bf16 h0 = (__bf16)vv[i][e];
+        const int va = (d4 + e) * kVRow + key * 2;
+        *reinterpret_cast<__bf16*>(vh_s + va) = h0;
+        *reinterpret_cast<__bf16*>(vl_s + va) = (__bf16)(vv[i][e] - (float)h0);
+      }
+    }
+    __syncthreads();
+    if (!wave_live) continue;  // wave-uniform; the barriers above are outside this branch
+
+    const int nch = (nk + 31) / 32;
+    for (int c = 0; c < nch; ++c) {
+      // S^T (32 keys x 32 queries)
+      f32x16 st;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) st[e] = 0.f;
+      const int key = c * 32 + r;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int ka = k_addr(key, 2 * s + hh);
+        st = mma3(*reinterpret_cast<const bf16x8*>(kh_s + ka), *reinterpret_cast<const bf16x8*>(kl_s + ka), qh[s],
+                  ql[s], st);
+      }
+      // online softmax over the keys of this lane's query column
+      float cmax = -FLT_MAX;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int kk = c * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+        if (kk >= nk) st[e] = -FLT_MAX;
+        cmax = fmaxf(cmax, st[e]);
+      }
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      const float mn = fmaxf(m, cmax);
+      const float corr = __expf(m - mn);
+      float ls = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int kk = c * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+        const float pe = kk < nk ? __expf(st[e] - mn) : 0.f;
+        st[e] = pe;
+        ls += pe;
+      }
+      l = l * corr + ls;
+      m = mn;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[t][e] *= corr;
+      // O^T (64 d x 32 queries) += V_c^T P; V^T row d = 32 t + r, keys c*32 + 16 s + 4 hh + {0..3, 8..11}
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 ph, pl;
+        const f32x4 p0 = {st[8 * s], st[8 * s + 1], st[8 * s + 2], st[8 * s + 3]};
+        const f32x4 p1 = {st[8 * s + 4], st[8 * s + 5], st[8 * s + 6], st[8 * s + 7]};
+        split8(p0, p1, ph, pl);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int va = (32 * t + r) * kVRow + (c * 32 + 16 * s + 4 * hh) * 2;
+          const bf16x4 a0 = *reinterpret_cast<const bf16x4*>(vh_s + va);
+          const bf16x4 a1 = *reinterpret_cast<const bf16x4*>(vh_s + va + 16);
+          const bf16x4 b0 = *reinterpret_cast<const bf16x4*>(vl_s + va);
+          const bf16x4 b1 = *reinterpret_cast<const bf16x4*>(vl_s + va + 16);
+          const bf16x8 vh = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+          const bf16x8 vl = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+          o[t] = mma3(vh, vl, ph, pl, o[t]);
+        }
+      }
+    }
+  }
+  if (!wave_live) return;
+  const float inv = 1.f / (l + __shfl_xor(l, 32, 64));
+  if (q < T) {
+    float* op = out + (rbase + q) * ldo + head * kDh + 4 * hh;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = {o[t][4 * g] * inv, o[t][4 * g + 1] * inv, o[t][4 * g + 2] * inv, o[t][4 * g + 3] * inv};
+        *reinterpret_cast<f32x4*>(op + 32 * t + 8 * g) = v;
+      }
+  }
+}
+
+}  // namespace
+
+void launch_attn(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s,
+                 const int* seg) {
+  WSP_CHECK(dh == kDh, "attn: head dim must be 64");
+  WSP_CHECK(B > 0 && T > 0 && H > 0 && ldq >= 3 * H * dh && ldq % 4 == 0 && ldo % 4 == 0, "attn: bad shape");
+  const dim3 grid((T + kQB - 1) / kQB, H, B);  // segmented: T = longest utterance
+  hipLaunchKernelGGL(attn_kernel, grid, dim3(512), kLds, s, qkv, ldq, out, ldo, T, H * dh, 1.f / sqrtf((float)dh),
+                     seg);
+  WSP_HIP(hipGetLastError());
+}
+
+}  // namespace wsp

@@ -207,6 +207,9 @@ void Model::set_option(const std::string& key, int value) {
   } else if (key == "res2_fused") {
     WSP_CHECK(value == 0 || value == 1, "res2_fused must be 0 or 1");
     impl->res2_fused = value;
+  } else if (key == "attn_lds") {
+    WSP_CHECK(value == 0 || value == 1, "attn_lds must be 0 or 1");
+    impl->attn_lds = value;
   } else if (key == "astp_fused") {
     WSP_CHECK(value == 0 || value == 1, "astp_fused must be 0 or 1");
     impl->astp_fused_on = value;

@@ -185,6 +185,7 @@ struct Model::Impl {
   std::vector<HLayer> h_layers;
   std::vector<float> h_fw;  // featurizer weight per hidden state
   int h_layer_sel = -1;     // s3prl `layer` (-1: softmax-weighted sum of all 13)
+  int attn_lds = 1;         // 1: attn.hip (K / V staged once in LDS), 0: hubert.hip mha_kernel (option "attn_lds")
   void build_hubert_params();
   void finalize_hubert();
   int hubert_cnn_frames(int N, int upto) const;
