@@ -64,18 +64,34 @@ HUBERT_TAGS = ("h_conv0", "h_cnn", "h_ln", "h_proj", "h_pos_conv", "h_qkv", "h_a
                "h_fc2", "h_cmn")
 
 
-def profiled_traffic(symbol: str, grid: int):
-    """HBM bytes per launch from the newest committed rocprofv3 PMC summary
-    (profiles/*_traffic.json, made by scripts/make_profile_summary.py)."""
+def profiled_record(symbol: str, grid: int):
+    """PMC record of a kernel launch geometry from the newest committed rocprofv3
+    summary (profiles/*_traffic.json, made by scripts/make_profile_summary.py):
+    HBM bytes per launch, MFMA utilisation (SQ_VALU_MFMA_BUSY_CYCLES over the SIMD
+    cycles of GRBM_GUI_ACTIVE) and the clock the launch ran at."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")),
+                   key=lambda f: (os.path.basename(f).startswith("r2"), os.path.getmtime(f)))
     for f in reversed(files):
         d = json.load(open(f))
         for key, v in d.items():
             sym, _, g = key.rpartition("|")
             if sym.startswith(symbol) and g == str(grid) and v.get("hbm_bytes"):
-                return v["hbm_bytes"], os.path.basename(f) + ":" + sym
+                return v, os.path.basename(f) + ":" + sym
     return None, None
+
+
+def profiled_traffic(symbol: str, grid: int):
+    rec, src = profiled_record(symbol, grid)
+    return (rec["hbm_bytes"], src) if rec else (None, None)
+
+
+def pmc_fields(symbol: str, grid: int) -> dict:
+    rec, _ = profiled_record(symbol, grid)
+    if not rec or rec.get("mfma_util") is None:
+        return {"mfma_util_pmc": None, "clock_ghz_pmc": None}
+    return {"mfma_util_pmc": round(rec["mfma_util"], 4),
+            "clock_ghz_pmc": round(rec["clock_ghz"], 3) if rec.get("clock_ghz") else None}
 
 
 def resnet_1x1_bytes_by_stage(arch: str, F: int, T: int, m: int = 32) -> dict:
@@ -500,7 +516,7 @@ def main():
                     "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"],
                     "mfma_dtype": "bf16 (3-term split, fp32 accumulate)" if x3 else "f32",
                     "mfma_work_factor": 3 if x3 else 1,
-                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4)}
+                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4), **pmc_fields(sym, grid)}
         elif k:
             C = 1024 if "c1024" in args.arch else 512
             M = B * T
@@ -518,7 +534,7 @@ def main():
                     "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"],
                     "mfma_dtype": "bf16 (3-term split, fp32 accumulate)" if x3 else "f32",
                     "mfma_work_factor": 3 if x3 else 1,
-                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4)}
+                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4), **pmc_fields(sym, grid)}
 
     gf = hubert_gflop_per_utt(N) + ecapa_gflop_per_utt(spec, T) if hubert else ecapa_gflop_per_utt(spec, T) \
         if args.arch.startswith("ECAPA") else simam_gflop_per_utt(spec, T) if simam else sum(

@@ -25,6 +25,9 @@ agg = defaultdict(lambda: defaultdict(list))
 for path in sorted(glob.glob(f"{src}/pmc*/p_counter_collection.csv")):
     for r in csv.DictReader(open(path)):
         agg[(r["Kernel_Name"], int(r["Grid_Size"]))][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if "End_Timestamp" in r and "Start_Timestamp" in r and r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+            agg[(r["Kernel_Name"], int(r["Grid_Size"]))]["_dur_ns"].append(
+                float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
 traffic = {}
 for (name, grid), d in agg.items():
     if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
@@ -34,7 +37,14 @@ for (name, grid), d in agg.items():
                                      "mfma_busy_cycles": (sum(d["SQ_VALU_MFMA_BUSY_CYCLES"]) / len(d["SQ_VALU_MFMA_BUSY_CYCLES"])
                                                           if "SQ_VALU_MFMA_BUSY_CYCLES" in d else None),
                                      "grbm_gui_active": (sum(d["GRBM_GUI_ACTIVE"]) / len(d["GRBM_GUI_ACTIVE"])
-                                                         if "GRBM_GUI_ACTIVE" in d else None)}
+                                                         if "GRBM_GUI_ACTIVE" in d else None),
+                                     "pmc_dur_ns": (sum(d["_dur_ns"]) / len(d["_dur_ns"]) if d.get("_dur_ns") else None)}
+        t = traffic[f"{name}|{grid}"]
+        if t["mfma_busy_cycles"] is not None and t["grbm_gui_active"]:
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs; SQ_VALU_MFMA_BUSY_CYCLES over the 1024 SIMDs
+            t["mfma_util"] = t["mfma_busy_cycles"] / (t["grbm_gui_active"] / 8 * 1024)
+            if t["pmc_dur_ns"]:
+                t["clock_ghz"] = t["grbm_gui_active"] / 8 / t["pmc_dur_ns"]
 json.dump(traffic, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
 log = os.path.join(src, "trace.log")
 if os.path.exists(log):
