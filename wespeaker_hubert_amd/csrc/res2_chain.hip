@@ -42,7 +42,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kPad = 4;  // image rows beyond each window edge (max dilation)
 
-template <int W, int R>
+template <int W, int R, int WNv>
 struct Geo {
   static constexpr int IR = R + 2 * kPad;          // image rows; row IR is the zero row
   static constexpr int RB = 2 * W;                 // bytes per image row and plane
@@ -50,8 +50,9 @@ struct Geo {
   static constexpr int KS = 3 * W / 16;            // 16-deep MFMA k-steps per conv (K = 3W)
   static constexpr int KC = W / 16;                // k-steps per tap
   static constexpr int WST = 64 * W;               // one k-step of W: W cols x 16 k x (hi, lo) bf16
-  static constexpr int WN = 2, WM = R / 64, TM = 2, TN = W / 64;
-  static constexpr int NW = WM * WN;
+  static constexpr int NW = R / 32;                // waves: 4 (R = 128) or 8 (R = 256)
+  static constexpr int WN = WNv, WM = NW / WN, TM = R / 32 / WM, TN = W / 32 / WN;
+  static_assert(TN >= 1 && TM >= 1, "res2 wave layout");
   static constexpr int NT = NW * 64;
   static constexpr int LDS = 2 * PLANE;
   // 16-B chunk swizzle: the 16 rows of a ds_read_b128 lane group land on 16
@@ -64,9 +65,9 @@ struct Geo {
 
 __device__ __forceinline__ unsigned short bf_bits(__bf16 x) { return __builtin_bit_cast(unsigned short, x); }
 
-template <int W, int R>
+template <int W, int R, int WNv>
 __global__ __launch_bounds__(2 * R, R == 128 ? 2 : 1) void res2_chain_kernel(const Res2Args p) {
-  using G = Geo<W, R>;
+  using G = Geo<W, R, WNv>;
   constexpr int TM = G::TM, TN = G::TN, NT = G::NT, IR = G::IR;
   static_assert(NT == 2 * R, "launch bounds assume 2R threads");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -159,11 +160,9 @@ __global__ __launch_bounds__(2 * R, R == 128 ? 2 : 1) void res2_chain_kernel(con
 
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(p.out);
   f32x16 acc[TM][TN];
-  // one 16-deep k-step g (tap, channel block kc) on the W fragments in (bh, bl),
-  // which are then reloaded with k-step g + 2
-  auto kstep = [&](int g, int tap, int kc, bf16x8 (&bh)[TN], bf16x8 (&bl)[TN]) {
-    bf16x8 ah[TM], al[TM];
-    const int q = kc * 2 + h;
+  // A fragments of k-step t of the current conv (tap t / KC, channel block t % KC)
+  auto read_a = [&](int t, bf16x8 (&ah)[TM], bf16x8 (&al)[TM]) {
+    const int tap = t / G::KC, q = (t % G::KC) * 2 + h;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int ar = tap == 0 ? arow[i][0] : tap == 1 ? arow[i][1] : arow[i][2];
@@ -172,6 +171,10 @@ __global__ __launch_bounds__(2 * R, R == 128 ? 2 : 1) void res2_chain_kernel(con
       ah[i] = *reinterpret_cast<const bf16x8*>(xhi + a);
       al[i] = *reinterpret_cast<const bf16x8*>(xlo + a);
     }
+  };
+  // one 16-deep k-step g on the fragments in (ah, al) and (bh, bl); the W
+  // fragments are then reloaded with k-step g + 2
+  auto mma = [&](int g, const bf16x8 (&ah)[TM], const bf16x8 (&al)[TM], bf16x8 (&bh)[TN], bf16x8 (&bl)[TN]) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -182,6 +185,7 @@ __global__ __launch_bounds__(2 * R, R == 128 ? 2 : 1) void res2_chain_kernel(con
       }
     wload(g + 2, bh, bl);
   };
+  bf16x8 a0h[TM], a0l[TM], a1h[TM], a1l[TM];
 
 #pragma unroll 1
   for (int step = 0; step < 7; ++step) {
@@ -192,11 +196,16 @@ __global__ __launch_bounds__(2 * R, R == 128 ? 2 : 1) void res2_chain_kernel(con
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    // KS is even: k-steps in pairs, W fragments alternating between two register sets
+    // KS is even: k-steps in pairs, A and W fragments alternating between two
+    // register sets — k-step t+1's A fragments are read from LDS while k-step t's
+    // MFMAs run (the image only changes between steps)
+    read_a(0, a0h, a0l);
 #pragma unroll 1
     for (int t = 0; t < G::KS - 2; t += 2) {
-      kstep(gb + t, t / G::KC, t % G::KC, wb0h, wb0l);
-      kstep(gb + t + 1, (t + 1) / G::KC, (t + 1) % G::KC, wb1h, wb1l);
+      read_a(t + 1, a1h, a1l);
+      mma(gb + t, a0h, a0l, wb0h, wb0l);
+      read_a(t + 2, a0h, a0l);
+      mma(gb + t + 1, a1h, a1l, wb1h, wb1l);
     }
     // the next conv's addend spx[step + 1] (accumulator layout: row per register,
     // col = lane & 31), issued two k-steps before the epilogue.  Row offsets are
@@ -223,8 +232,9 @@ __global__ __launch_bounds__(2 * R, R == 128 ? 2 : 1) void res2_chain_kernel(con
         }
       }
     }
-    kstep(gb + G::KS - 2, 2, G::KC - 2, wb0h, wb0l);
-    kstep(gb + G::KS - 1, 2, G::KC - 1, wb1h, wb1l);
+    read_a(G::KS - 1, a1h, a1l);
+    mma(gb + G::KS - 2, a0h, a0l, wb0h, wb0l);
+    mma(gb + G::KS - 1, a1h, a1l, wb1h, wb1l);
     __syncthreads();  // every wave is done reading X_step
 
     // ---- epilogue: sp = BN(ReLU(acc + b)); owned rows -> out; X_{step+1} -> LDS
@@ -273,17 +283,22 @@ bool res2_chain_supported(int w, int dil) { return (w == 64 || w == 128) && dil 
 
 static int res2_rows(int variant) { return (variant & 1) ? 256 : 128; }
 
-template <int W, int R>
+template <int W, int R, int WN>
 void launch_res2_k(const Res2Args& p, int nblk, hipStream_t s) {
-  hipLaunchKernelGGL((res2_chain_kernel<W, R>), dim3(nblk), dim3(Geo<W, R>::NT), (Geo<W, R>::LDS), s, p);
+  hipLaunchKernelGGL((res2_chain_kernel<W, R, WN>), dim3(nblk), dim3(Geo<W, R, WN>::NT),
+                     (Geo<W, R, WN>::LDS), s, p);
 }
 
 template <int W>
 void launch_res2_w(const Res2Args& p, int nblk, hipStream_t s) {
-  if (p.variant & 1)
-    launch_res2_k<W, 256>(p, nblk, s);
-  else
-    launch_res2_k<W, 128>(p, nblk, s);
+  if (p.variant & 1) {
+    launch_res2_k<W, 256, 2>(p, nblk, s);
+  } else if (p.variant & 2) {
+    if constexpr (W == 128) launch_res2_k<W, 128, 4>(p, nblk, s);  // 1 x 4 waves: 128 rows x 32 channels
+    else launch_res2_k<W, 128, 2>(p, nblk, s);
+  } else {
+    launch_res2_k<W, 128, 2>(p, nblk, s);
+  }
 }
 
 void launch_res2_chain(const Res2Args& p, int w, hipStream_t s) {
