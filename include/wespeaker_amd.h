@@ -126,14 +126,27 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
                                int total_frames, float* embed, void* workspace, size_t workspace_bytes,
                                void* stream);
 
-/* Runtime options (any time after create):
- *   "precision"  1 = bf16x3 split MFMA (default; fp32-class accuracy),
- *                0 = exact f32 MFMA
- *   "x3_variant" bf16x3 block tile: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves),
- *                2 = LDS-DMA staged 256x128 where supported, 3 = 128x128 with
- *                swizzled 64-B LDS rows, 4 = 256x128 swizzled (default)
- *   "layer"      HuBERT front end only, before finalize: -1 = weighted sum of all
- *                hidden states (default), k = hidden state k alone (s3prl.py:84-87) */
+/* Runtime options (any time after create unless noted):
+ *   "precision"    1 = bf16x3 split MFMA (default; fp32-class accuracy),
+ *                  0 = exact f32 MFMA (ECAPA-TDNN and HuBERT)
+ *   "streams"      1..8: the batch's utterances are split into this many contiguous
+ *                  ranges forwarded on concurrent HIP streams (forked from and joined
+ *                  back to the caller's stream; each range has its own workspace
+ *                  slice, so query the workspace size after setting it); results are
+ *                  bit-identical to 1.  Default 2 for ResNet / SimAM-ResNet / HuBERT,
+ *                  1 for ECAPA-TDNN; segmented ECAPA batches always run as one range
+ *   "x3_variant"   bf16x3 conv-GEMM tile: 0 = 128x128, 1 = 256x128, 3 = 128x128 with
+ *                  swizzled LDS rows (ResNet default), 4 = 256x128 swizzled,
+ *                  5 = 256x256 where N % 256 == 0 (default), 6 = 256x128 one staging
+ *                  set, 2 / 9 = LDS-DMA staged variants where supported
+ *   "res2_fused"   1 = one res2_chain launch per SE_Res2Block (default), 0 = 7 GEMMs
+ *   "res2_variant" res2_chain tile: 0 = 128 rows, 2 waves on N (default), 1 = 256 rows,
+ *                  2 = 128 rows, 4 waves on N (C = 128 only)
+ *   "astp_fused"   1 = ASTP linear2 + softmax statistics in one kernel (default)
+ *   "attn_lds"     HuBERT: 1 = K / V staged once per 256-key block in LDS (default)
+ *   "in_planes"    SimAM-ResNet, before the weights: 32 or 64
+ *   "layer"        HuBERT front end only, before finalize: -1 = weighted sum of all
+ *                  hidden states (default), k = hidden state k alone (s3prl.py:84-87) */
 int wsp_model_set_option(wsp_model* m, const char* key, int value);
 
 /* Per-kernel-class timing with HIP events recorded on the launch stream

@@ -353,7 +353,14 @@ size_t Model::frontend_workspace_bytes(int B, int N) const {
 size_t Model::frontend_workspace_bytes_segments(int B, const int* lens) const {
   WSP_CHECK(impl->hubert, "frontend_workspace_bytes: not a front-end handle");
   WSP_CHECK(B > 0 && lens, "HuBERT needs B >= 1 utterances");
-  return impl->hubert_ws_floats(impl->hubert_plan(B, lens), nullptr) * sizeof(float) + 256;
+  const int ns = impl->nsub(B);
+  size_t bytes = 256;
+  for (int i = 0; i < ns; ++i) {
+    const int b0 = B * i / ns, b1 = B * (i + 1) / ns;
+    bytes += (impl->hubert_ws_floats(impl->hubert_plan(b1 - b0, lens + b0), nullptr) * sizeof(float) + 255) &
+             ~size_t(255);
+  }
+  return bytes;
 }
 
 void Model::forward_frontend(const float* wav, int B, int N, float* feats, int cmn, void* ws, size_t ws_bytes,
@@ -369,11 +376,36 @@ void Model::forward_frontend_segments(const float* wav, int B, const int* lens, 
   WSP_CHECK(m.hubert, "forward_frontend: not a front-end handle");
   WSP_CHECK(m.finalized, "forward before finalize");
   WSP_CHECK(B > 0 && lens, "HuBERT needs B >= 1 utterances");
-  const HubertPlan pl = m.hubert_plan(B, lens);
-  WSP_CHECK(ws_bytes >= m.hubert_ws_floats(pl, nullptr) * sizeof(float) + 256, "workspace too small");
-  if (frame_offsets) std::copy(pl.offs.begin() + B + 1, pl.offs.begin() + 2 * (B + 1), frame_offsets);
-  float* wsf = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
-  m.forward_hubert(wav, pl, feats, cmn, wsf, s);
+  WSP_CHECK(ws_bytes >= frontend_workspace_bytes_segments(B, lens), "workspace too small");
+  // utterance ranges on concurrent streams (option "streams"); each range's plan is
+  // relative to its first sample / output frame
+  const int ns = m.nsub(B);
+  std::vector<HubertPlan> pls(ns);
+  for (int i = 0; i < ns; ++i) {
+    const int b0 = B * i / ns, b1 = B * (i + 1) / ns;
+    pls[i] = m.hubert_plan(b1 - b0, lens + b0);
+  }
+  if (frame_offsets) {
+    frame_offsets[0] = 0;
+    int b = 0;
+    for (int i = 0; i < ns; ++i) {
+      const HubertPlan& pl = pls[i];
+      const int base = frame_offsets[b];
+      for (int j = 1; j <= pl.B; ++j) frame_offsets[b + j] = base + pl.offs[pl.B + 1 + j];
+      b += pl.B;
+    }
+  }
+  char* wsb = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+  if (ns > 1) m.fork(s, ns);
+  size_t sample0 = 0, frame0 = 0;
+  for (int i = 0; i < ns; ++i) {
+    const HubertPlan& pl = pls[i];
+    m.forward_hubert(wav + sample0, pl, feats + frame0 * kHidden, cmn, reinterpret_cast<float*>(wsb), m.sub(s, i));
+    wsb += (m.hubert_ws_floats(pl, nullptr) * sizeof(float) + 255) & ~size_t(255);
+    for (int b = B * i / ns; b < B * (i + 1) / ns; ++b) sample0 += lens[b];
+    frame0 += pl.Mout;
+  }
+  if (ns > 1) m.join(s, ns);
 }
 
 }  // namespace wsp

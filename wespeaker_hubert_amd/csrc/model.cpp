@@ -23,6 +23,8 @@ Model::~Model() {
       (void)hipEventDestroy(e.first);
       (void)hipEventDestroy(e.second);
     }
+  for (auto t : impl->sub_st) (void)hipStreamDestroy(t);
+  for (auto e : impl->sub_ev) (void)hipEventDestroy(e);
   delete impl;
 }
 
@@ -58,6 +60,7 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
     WSP_CHECK(feat_dim >= 8, "ResNet feat_dim must be >= 8");
     m.ecapa = false;
     m.x3_variant = 3;  // HBM-bound 1x1 convs: two 128 x 128 blocks per CU (+4 % over variant 4)
+    m.streams = 2;     // two utterance ranges in flight: ResNet293 C3 +8.6 %
     m.bottleneck = it->second.first;
     for (int i = 0; i < 4; ++i) m.nblocks[i] = it->second.second[i];
     m.build_resnet_params();
@@ -71,6 +74,7 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
     m.simam = true;
     m.bottleneck = false;
     m.x3_variant = 5;  // MFMA-bound 3x3 convs (K = 9C): wide tiles where N % 256 == 0 (+6 % over variant 3)
+    m.streams = 2;     // SimAM-ResNet100 +3.8 %
     m.m_ch = 64;
     const int nb34[4] = {3, 4, 6, 3}, nb100[4] = {6, 16, 24, 3};
     for (int i = 0; i < 4; ++i) m.nblocks[i] = arch == "SimAM_ResNet34_ASP" ? nb34[i] : nb100[i];
@@ -82,6 +86,7 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
     m.ecapa = false;
     m.hubert = true;
     m.feat_dim = 1;
+    m.streams = 2;  // HuBERT + ECAPA C4 chain +2.6 %
     m.build_hubert_params();
   } else {
     throw InvalidArg{"unsupported arch " + arch};
@@ -131,12 +136,20 @@ void Model::finalize() {
 int Model::embed_dim() const { return impl->embed_dim; }
 int Model::feat_dim() const { return impl->feat_dim; }
 
+// workspace of one sub-batch of B utterances, 256-byte granules
+size_t Model::Impl::ws_bytes_one(int B, int T) const {
+  const size_t f = ecapa   ? ecapa_ws_floats(B, (size_t)B * T, nullptr)
+                   : simam ? simam_ws_floats(B, T, nullptr)
+                           : resnet_ws_floats(B, T, nullptr);
+  return (f * sizeof(float) + 255) & ~size_t(255);
+}
+
 size_t Model::workspace_bytes(int B, int T) const {
   WSP_CHECK(!impl->hubert, "HuBERT handle: use the front-end workspace query");
-  const size_t f = impl->ecapa   ? impl->ecapa_ws_floats(B, (size_t)B * T, nullptr)
-                   : impl->simam ? impl->simam_ws_floats(B, T, nullptr)
-                                 : impl->resnet_ws_floats(B, T, nullptr);
-  return f * sizeof(float) + 256;
+  const int ns = impl->nsub(B);
+  size_t bytes = 256;
+  for (int i = 0; i < ns; ++i) bytes += impl->ws_bytes_one(B * (i + 1) / ns - B * i / ns, T);
+  return bytes;
 }
 
 void Model::forward(const float* feats, int B, int T, float* embed, void* ws, size_t ws_bytes,
@@ -147,18 +160,26 @@ void Model::forward(const float* feats, int B, int T, float* embed, void* ws, si
   WSP_CHECK(B > 0 && T > 1, "forward needs B >= 1 and T >= 2 frames");
   WSP_CHECK((size_t)B * T < (1u << 31), "B*T too large");
   WSP_CHECK(ws_bytes >= workspace_bytes(B, T), "workspace too small");
-  float* wsf = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
-  if (m.ecapa) {
-    m.forward_ecapa(feats, B, T, embed, wsf, s);
-  } else {
-    WSP_CHECK(m.precision == 1, "ResNet runs on the bf16x3 kernels only (precision=1)");
-    if (m.simam) {
-      WSP_CHECK((T + 7) / 8 >= 2, "SimAM-ResNet needs >= 2 frames after the three stride-2 stages");
-      m.forward_simam(feats, B, T, embed, wsf, s);
-    } else {
-      m.forward_resnet(feats, B, T, embed, wsf, s);
-    }
+  WSP_CHECK(m.ecapa || m.precision == 1, "ResNet runs on the bf16x3 kernels only (precision=1)");
+  WSP_CHECK(!m.simam || (T + 7) / 8 >= 2, "SimAM-ResNet needs >= 2 frames after the three stride-2 stages");
+  char* wsb = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+  const int ns = m.nsub(B);
+  if (ns > 1) m.fork(s, ns);
+  for (int i = 0; i < ns; ++i) {
+    const int b0 = B * i / ns, nb = B * (i + 1) / ns - b0;
+    const float* f = feats + (size_t)b0 * T * m.feat_dim;
+    float* e = embed + (size_t)b0 * m.embed_dim;
+    float* wsf = reinterpret_cast<float*>(wsb);
+    const hipStream_t si = m.sub(s, i);
+    if (m.ecapa)
+      m.forward_ecapa(f, nb, T, e, wsf, si);
+    else if (m.simam)
+      m.forward_simam(f, nb, T, e, wsf, si);
+    else
+      m.forward_resnet(f, nb, T, e, wsf, si);
+    wsb += m.ws_bytes_one(nb, T);
   }
+  if (ns > 1) m.join(s, ns);
 }
 
 size_t Model::workspace_bytes_segments(int B, int M) const {
@@ -213,6 +234,9 @@ void Model::set_option(const std::string& key, int value) {
   } else if (key == "astp_fused") {
     WSP_CHECK(value == 0 || value == 1, "astp_fused must be 0 or 1");
     impl->astp_fused_on = value;
+  } else if (key == "streams") {
+    WSP_CHECK(value >= 1 && value <= 8, "streams must be 1..8");
+    impl->streams = value;
   } else if (key == "res2_variant") {
     impl->res2_variant = value;
   } else if (key == "x3_variant") {

@@ -203,6 +203,37 @@ struct Model::Impl {
   // conv_gemm_x3 variant behind x3_variant (the DMA selections 2 / 9 fall back to 5)
   int x3_base() const { return (x3_variant == 2 || x3_variant >= 7) ? 5 : x3_variant; }
 
+  // concurrent sub-batches (option "streams"): the batch's utterances are split
+  // into `streams` contiguous ranges, each forwarded on its own HIP stream over its
+  // own workspace slice, so one range's HBM-bound kernels run beside the other's
+  // MFMA-bound GEMMs; the caller's stream forks to and joins them with events.
+  int streams = 1;
+  std::vector<hipStream_t> sub_st;  // streams 1.. (range 0 runs on the caller's stream)
+  std::vector<hipEvent_t> sub_ev;   // [0] fork, [i] join of range i
+  int nsub(int B) const { return std::max(1, std::min(streams, B)); }
+  size_t ws_bytes_one(int B, int T) const;
+  hipStream_t sub(hipStream_t s, int i) const { return i == 0 ? s : sub_st[i - 1]; }
+  void fork(hipStream_t s, int ns) {
+    while ((int)sub_st.size() < ns - 1) {
+      hipStream_t t;
+      WSP_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
+      sub_st.push_back(t);
+    }
+    while ((int)sub_ev.size() < ns) {
+      hipEvent_t e;
+      WSP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      sub_ev.push_back(e);
+    }
+    WSP_HIP(hipEventRecord(sub_ev[0], s));
+    for (int i = 1; i < ns; ++i) WSP_HIP(hipStreamWaitEvent(sub_st[i - 1], sub_ev[0], 0));
+  }
+  void join(hipStream_t s, int ns) {
+    for (int i = 1; i < ns; ++i) {
+      WSP_HIP(hipEventRecord(sub_ev[i], sub_st[i - 1]));
+      WSP_HIP(hipStreamWaitEvent(s, sub_ev[i], 0));
+    }
+  }
+
   // profiling
   bool prof = false;
   std::map<std::string, ProfEntry> prof_map;

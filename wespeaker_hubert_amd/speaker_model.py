@@ -152,7 +152,9 @@ class _HipHandle:
         return self._ws
 
     def set_option(self, key: str, value: int):
-        """'precision': 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA."""
+        """Runtime option of the handle (include/wespeaker_amd.h lists them), e.g.
+        'precision': 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA;
+        'streams': utterance ranges forwarded on concurrent HIP streams."""
         self._options[key] = int(value)
         if key in self._pre_finalize:
             self._release()  # rebuilt with the option on the next .to()/forward
