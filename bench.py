@@ -438,6 +438,10 @@ def main():
         exact = {"value": round(world * B * n_f / e_f, 2), "steps": n_f,
                  "ms_per_step": round(e_f / n_f * 1e3, 3), "dtype": "f32 (v_mfma_f32_32x32x2_f32)"}
 
+    # concurrent sub-batch streams in effect (model option "streams"; front end for C4):
+    # with more than one, per-launch durations are measured while another range's
+    # kernels share the GPU, so per-kernel roofline fractions read low
+    streams = max(m.get_option("streams") for m in (model, fe) if m is not None)
     kernels, roof = {}, None
     if not args.no_profile:
         queries = [(model, t) for t in HEAD_TAGS] + ([(fe, t) for t in HUBERT_TAGS] if fe is not None else [])
@@ -499,7 +503,11 @@ def main():
                     "traffic_source": ",".join(sorted(traffic_srcs)) or None,
                     "traffic_note": "PMC HBM bytes of all 1x1 launches of a step (FETCH_SIZE x2 + WRITE_SIZE)",
                     "algorithmic_bytes": byts, "launches_per_step": kr["launches_per_step"],
-                    "ms_per_step": kr["ms_per_step"]}
+                    "ms_per_step": kr["ms_per_step"],
+                    "concurrent_streams": streams}
+            if streams > 1:
+                roof["note"] = ("launch durations measured beside the other utterance range's kernels "
+                                "(option streams); --opt streams=1 gives the standalone rate")
         elif k and hubert:
             Th = (N - 400) // 320 + 1  # HuBERT conv frames (249 for 5 s)
             M, Nn, K = B * Th, 3072, 768
@@ -560,7 +568,8 @@ def main():
                                 f"{args.seconds:g}s 16kHz utts" if hubert else
                                 f"{args.arch} fbank80 extract, {args.seconds:g}s 16kHz utts"),
                    "arch": args.arch, "batch_per_gpu": B, "global_batch": B * world,
-                   "samples_per_utt": N, "frames": T, "parallelism": f"dp{world}"},
+                   "samples_per_utt": N, "frames": T, "parallelism": f"dp{world}",
+                   "streams": streams},
         "model_tflops": round(value * gf / 1e3, 2),
         "gflop_per_utt": round(gf, 3),
         "roofline": roof,

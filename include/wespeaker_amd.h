@@ -148,6 +148,8 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *   "layer"        HuBERT front end only, before finalize: -1 = weighted sum of all
  *                  hidden states (default), k = hidden state k alone (s3prl.py:84-87) */
 int wsp_model_set_option(wsp_model* m, const char* key, int value);
+/* The current value of a runtime option above (the per-architecture default until set). */
+int wsp_model_get_option(const wsp_model* m, const char* key, int* value);
 
 /* Per-kernel-class timing with HIP events recorded on the launch stream
  * around every launch (used by bench.py for the roofline figure). */

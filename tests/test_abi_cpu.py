@@ -81,3 +81,29 @@ def test_unknown_arch_is_an_error():
     lib = _lib.load()
     h = ctypes.c_void_p()
     assert lib.wsp_model_create(b"NOPE", 80, 192, 0, 0, ctypes.byref(h)) != 0
+
+
+def test_option_defaults_and_streams_workspace():
+    """Host-only: per-architecture option defaults (wsp_model_get_option) and the
+    workspace of a split batch ("streams": one 256-B-granular slice per range)."""
+    lib = _lib.load()
+    v, b1, b2 = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_size_t()
+    for arch, feat, emb, want in ((b"ECAPA_TDNN_c512", 80, 192, 1), (b"ResNet34", 80, 256, 2),
+                                  (b"HuBERT_base", 1, 768, 2)):
+        h = ctypes.c_void_p()
+        assert lib.wsp_model_create(arch, feat, emb, 0, 0, ctypes.byref(h)) == 0
+        try:
+            assert lib.wsp_model_get_option(h, b"streams", ctypes.byref(v)) == 0 and v.value == want
+            assert lib.wsp_model_get_option(h, b"precision", ctypes.byref(v)) == 0 and v.value == 1
+            assert lib.wsp_model_get_option(h, b"nope", ctypes.byref(v)) != 0
+            assert lib.wsp_model_set_option(h, b"streams", 0) != 0
+            if arch != b"HuBERT_base":
+                assert lib.wsp_model_set_option(h, b"streams", 1) == 0
+                assert lib.wsp_model_workspace_bytes(h, 6, 200, ctypes.byref(b1)) == 0
+                assert lib.wsp_model_set_option(h, b"streams", 3) == 0
+                assert lib.wsp_model_get_option(h, b"streams", ctypes.byref(v)) == 0 and v.value == 3
+                assert lib.wsp_model_workspace_bytes(h, 6, 200, ctypes.byref(b2)) == 0
+                # three 2-utterance slices: about the 6-utterance workspace (per-slice fixed parts)
+                assert b1.value // 2 < b2.value <= b1.value + 3 * 65536
+        finally:
+            lib.wsp_model_destroy(h)

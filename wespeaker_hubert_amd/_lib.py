@@ -41,6 +41,7 @@ SIGNATURES = {
     "wsp_model_forward_segments": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                            c_size_t, c_void_p]),
     "wsp_model_set_option": (c_int, [c_void_p, c_char_p, c_int]),
+    "wsp_model_get_option": (c_int, [c_void_p, c_char_p, POINTER(c_int)]),
     "wsp_frontend_out_frames": (c_int, [c_void_p, c_int, POINTER(c_int)]),
     "wsp_frontend_workspace_bytes": (c_int, [c_void_p, c_int, c_int, POINTER(c_size_t)]),
     "wsp_frontend_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_size_t,

@@ -227,6 +227,13 @@ int wsp_model_set_option(wsp_model* m, const char* key, int value) {
   });
 }
 
+int wsp_model_get_option(const wsp_model* m, const char* key, int* value) {
+  WSP_GUARD({
+    WSP_CHECK(m && key && value, "null argument");
+    *value = m->m.get_option(key);
+  });
+}
+
 int wsp_model_profile(wsp_model* m, int enable) {
   WSP_GUARD({
     WSP_CHECK(m, "null model");

@@ -1,0 +1,20 @@
+// conv_gemm_x3 tile family instantiations (see conv_gemm_x3_impl.h).
+#include "conv_gemm_x3_impl.h"
+
+namespace wsp {
+namespace x3 {
+
+void t_4x1_1x1(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s) {
+  launch_x3_tile<4, 1, 1, 1>(p, h, l, s);
+}
+
+void t_4x1_1x2(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s) {
+  launch_x3_tile<4, 1, 1, 2>(p, h, l, s);
+}
+
+void t_8x1_1x2_sw(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s) {
+  launch_x3_tile<8, 1, 1, 2, true>(p, h, l, s);
+}
+
+}  // namespace x3
+}  // namespace wsp

@@ -247,6 +247,20 @@ void Model::set_option(const std::string& key, int value) {
   }
 }
 
+int Model::get_option(const std::string& key) const {
+  const Impl& m = *impl;
+  if (key == "precision") return m.precision;
+  if (key == "streams") return m.streams;
+  if (key == "layer") return m.h_layer_sel;
+  if (key == "in_planes") return m.m_ch;
+  if (key == "res2_fused") return m.res2_fused;
+  if (key == "attn_lds") return m.attn_lds;
+  if (key == "astp_fused") return m.astp_fused_on;
+  if (key == "res2_variant") return m.res2_variant;
+  if (key == "x3_variant") return m.x3_variant;
+  throw InvalidArg{"unknown option " + key};
+}
+
 void Model::profile_query(const std::string& tag, int* launches, double* total_ms, double* flops) {
   // `tag` names one kernel class or, as a prefix "tag.", every sub-class under it
   // (e.g. "res_conv1x1" = "res_conv1x1.c1.L1" + ...).  Launches of the current /

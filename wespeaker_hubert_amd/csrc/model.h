@@ -40,6 +40,7 @@ class Model {
                         hipStream_t s);
   void profile(bool on);
   void set_option(const std::string& key, int value);
+  int get_option(const std::string& key) const;
   void profile_query(const std::string& tag, int* launches, double* total_ms, double* flops);
 
   struct Impl;

@@ -235,19 +235,23 @@ __global__ __launch_bounds__(256) void residual_scale_kernel(const f32x4* __rest
   const int r1 = min(M, r0 + kRSRows);
   for (int c4 = threadIdx.x % tpr; c4 < C4; c4 += tpr) {
     int r = r0 + sub;
-    for (; r + 3 * rpp < r1; r += 4 * rpp) {
-      f32x4 xv[4], hv[4], gv[4];
+    // 8 rows per pass: 16 float4 loads in flight per thread
+    for (; r + 7 * rpp < r1; r += 8 * rpp) {
+      f32x4 xv[8], hv[8], gv[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
+        const long i = (long)(r + u * rpp) * C4 + c4;
+        xv[u] = __builtin_nontemporal_load(x + i);
+        hv[u] = __builtin_nontemporal_load(h + i);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
         const int row = r + u * rpp;
         const int b = seg ? seg_of(seg, nseg, row) : row / T;
-        const long i = (long)row * C4 + c4;
-        xv[u] = x[i];
-        hv[u] = h[i];
         gv[u] = *reinterpret_cast<const f32x4*>(g + ((long)b * C4 + c4) * 4);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) out[(long)(r + u * rpp) * C4 + c4] = xv[u] + hv[u] * gv[u];
+      for (int u = 0; u < 8; ++u) out[(long)(r + u * rpp) * C4 + c4] = xv[u] + hv[u] * gv[u];
     }
     for (; r < r1; r += rpp) {
       const int b = seg ? seg_of(seg, nseg, r) : r / T;

@@ -161,6 +161,13 @@ class _HipHandle:
         elif self._handle is not None:
             _lib.check(_lib.load().wsp_model_set_option(self._handle, key.encode(), int(value)), "set_option")
 
+    def get_option(self, key: str) -> int:
+        """Value of a runtime option on the device handle (set or per-architecture default)."""
+        self._need()
+        v = ctypes.c_int(0)
+        _lib.check(_lib.load().wsp_model_get_option(self._handle, key.encode(), ctypes.byref(v)), "get_option")
+        return int(v.value)
+
     # ----------------------------------------------------------- profile --
     def profile(self, enable: bool):
         self._need()
