@@ -142,7 +142,10 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *   "res2_fused"   1 = one res2_chain launch per SE_Res2Block (default), 0 = 7 GEMMs
  *   "res2_variant" res2_chain tile: 0 = 128 rows, 2 waves on N (default), 1 = 256 rows,
  *                  2 = 128 rows, 4 waves on N (C = 128 only)
- *   "astp_fused"   1 = ASTP linear2 + softmax statistics in one kernel (default)
+ *   "astp_fused"   ASTP linear2 + softmax statistics in one kernel: 1 = 128 channels per
+ *                  block, 2 = 256 channels with att chunks shared through LDS-DMA, 3 = 2 with
+ *                  W2 in registers and a deeper ring (default; all three bit-identical);
+ *                  0 = linear2 GEMM + separate pooling kernel
  *   "attn_lds"     HuBERT: 1 = K / V staged once per 256-key block in LDS (default)
  *   "in_planes"    SimAM-ResNet, before the weights: 32 or 64
  *   "layer"        HuBERT front end only, before finalize: -1 = weighted sum of all

@@ -24,8 +24,9 @@ struct AstpArgs {
   const float* bias2;
   float var_floor;
   float* out;
+  int variant = 1;  // 1: 128 channels / 4 waves per block; 2: 256 / 8 waves, att chunks shared via LDS-DMA
 };
-bool astp_fused_supported(int C, int K);
+bool astp_fused_supported(int C, int K, int variant = 1);
 void launch_astp_fused(const AstpArgs& p, hipStream_t s);
 
 }  // namespace wsp

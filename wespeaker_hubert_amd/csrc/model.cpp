@@ -232,7 +232,7 @@ void Model::set_option(const std::string& key, int value) {
     WSP_CHECK(value == 0 || value == 1, "attn_lds must be 0 or 1");
     impl->attn_lds = value;
   } else if (key == "astp_fused") {
-    WSP_CHECK(value == 0 || value == 1, "astp_fused must be 0 or 1");
+    WSP_CHECK(value >= 0 && value <= 3, "astp_fused must be 0 (unfused) or 1..3 (fused kernel variant)");
     impl->astp_fused_on = value;
   } else if (key == "streams") {
     WSP_CHECK(value >= 1 && value <= 8, "streams must be 1..8");

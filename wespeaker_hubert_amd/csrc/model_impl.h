@@ -143,7 +143,9 @@ struct Model::Impl {
   int res2_variant = 0;  // res2_chain.hip kernel variant (option "res2_variant")
   ConvW conv, pool1, pool2;
   void* pool2_frag = nullptr;  // pool.linear2 in MFMA B-fragment order for astp_fused.hip
-  int astp_fused_on = 1;       // 0: linear2 GEMM + separate pooling kernel (option "astp_fused")
+  // 0: linear2 GEMM + separate pooling kernel; 1..3: astp_fused.hip variant (option "astp_fused";
+  // 3 = 256 channels per block, att chunks two ahead in an LDS-DMA ring, W2 in VGPRs: C2 0.465 -> 0.31 ms)
+  int astp_fused_on = 3;
   LinW pool1_ctx;
   LinW head;
 
@@ -1108,7 +1110,7 @@ struct Model::Impl {
     }
     if (precision == 1 && astp_fused_on) {
       // linear2 + softmax over frames + attentive mean / std in one pass (astp_fused.hip)
-      AstpArgs a{att, xp, 1536, B, T, 1536, seg, pool2_frag, pool2.bias, 1e-7f, pooled};
+      AstpArgs a{att, xp, 1536, B, T, 1536, seg, pool2_frag, pool2.bias, 1e-7f, pooled, astp_fused_on};
       run("astp", 2.0 * M * 1536 * 128, s, [&] { launch_astp_fused(a, s); });
     } else {
       gemm("pool_linear2", pool2, att, 128, logit, 1536, M, T, 1, 0, kActNone, s);
