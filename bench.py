@@ -163,7 +163,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=None, help="per GPU (default 256 ECAPA, 128 ResNet, 64 HuBERT)")
+    ap.add_argument("--batch", type=int, default=None, help="per GPU (default 256 ECAPA and HuBERT + ECAPA, 128 ResNet)")
     ap.add_argument("--arch", default="ECAPA_TDNN_c1024",
                     help=f"ECAPA_TDNN_*, ResNet*, or {HUBERT_ARCH} (wav -> HuBERT -> CMN -> ECAPA)")
     ap.add_argument("--seconds", type=float, default=5.0)
@@ -334,7 +334,9 @@ def main():
     hubert = args.arch == HUBERT_ARCH
     simam = args.arch.startswith("SimAM")
     resnet_like = args.arch.startswith("ResNet") or simam
-    B = args.batch or (64 if hubert else 128 if resnet_like else 256)
+    # C4 per GPU: 256 utterances like C2 (fc2 / out_proj have 3 column tiles of 256:
+    # 64 utterances fill 189 of the 256 CUs; 256 fill 2.9 rounds; +12.5 % over 64)
+    B = args.batch or (128 if resnet_like else 256)
     N = int(round(args.seconds * 16000))
     emb_dim = 256 if resnet_like else 192
     head_arch = "ECAPA_TDNN_GLOB_c512" if hubert else args.arch
@@ -451,7 +453,8 @@ def main():
                 avg = ms / n
                 kernels[tag] = {"launches_per_step": n // args.steps, "avg_ms": round(avg, 4),
                                 "ms_per_step": round(ms / args.steps, 4),
-                                "tflops": round(fl / (avg * 1e-3) / 1e12, 2) if fl else None}
+                                "tflops": round(fl / (avg * 1e-3) / 1e12, 2) if fl else None,
+                                "flops_per_launch": fl or None}
         k = kernels.get("h_fc1") if hubert else kernels.get("conv1x1_CxC")
         kr = kernels.get("res_conv1x1") if args.arch.startswith("ResNet") else None
         k3 = kernels.get("res_conv3x3") if simam else None
@@ -510,7 +513,7 @@ def main():
                                 "(option streams); --opt streams=1 gives the standalone rate")
         elif k and hubert:
             Th = (N - 400) // 320 + 1  # HuBERT conv frames (249 for 5 s)
-            M, Nn, K = B * Th, 3072, 768
+            M, Nn, K = B * Th // streams, 3072, 768  # rows per launch (one utterance range)
             flops = 2.0 * M * Nn * K
             ach = flops / (k["avg_ms"] * 1e-3) / 1e12
             x3 = args.precision == 1
@@ -524,10 +527,11 @@ def main():
                     "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"],
                     "mfma_dtype": "bf16 (3-term split, fp32 accumulate)" if x3 else "f32",
                     "mfma_work_factor": 3 if x3 else 1,
-                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4), **pmc_fields(sym, grid)}
+                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4), **pmc_fields(sym, grid),
+                    "concurrent_streams": streams}
         elif k:
             C = 1024 if "c1024" in args.arch else 512
-            M = B * T
+            M = B * T // streams             # rows per launch (one utterance range)
             flops = 2.0 * M * C * C          # algorithmic: 2*M*N*K, M = B*T frames
             ach = flops / (k["avg_ms"] * 1e-3) / 1e12
             x3 = args.precision == 1
@@ -542,7 +546,11 @@ def main():
                     "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"],
                     "mfma_dtype": "bf16 (3-term split, fp32 accumulate)" if x3 else "f32",
                     "mfma_work_factor": 3 if x3 else 1,
-                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4), **pmc_fields(sym, grid)}
+                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4), **pmc_fields(sym, grid),
+                    "concurrent_streams": streams}
+        if roof is not None and streams > 1 and "note" not in roof:
+            roof["note"] = ("launch durations measured beside the other utterance range's kernels "
+                            "(option streams); --opt streams=1 gives the standalone rate")
 
     gf = hubert_gflop_per_utt(N) + ecapa_gflop_per_utt(spec, T) if hubert else ecapa_gflop_per_utt(spec, T) \
         if args.arch.startswith("ECAPA") else simam_gflop_per_utt(spec, T) if simam else sum(
