@@ -64,14 +64,22 @@ HUBERT_TAGS = ("h_conv0", "h_cnn", "h_ln", "h_proj", "h_pos_conv", "h_qkv", "h_a
                "h_fc2", "h_cmn")
 
 
+# workload tag of the profile summaries that may describe this run's kernels
+# (profiles/r<N>_<tag>_traffic.json): the same template symbol and grid can occur in
+# two workloads (C4's fc1 at B = 256 has conv_cat's C2 grid), so only the run's own
+# workload's summaries are searched
+PROFILE_TAG = "c2"
+
+
 def profiled_record(symbol: str, grid: int):
     """PMC record of a kernel launch geometry from the newest committed rocprofv3
-    summary (profiles/*_traffic.json, made by scripts/make_profile_summary.py):
-    HBM bytes per launch, MFMA utilisation (SQ_VALU_MFMA_BUSY_CYCLES over the SIMD
-    cycles of GRBM_GUI_ACTIVE) and the clock the launch ran at."""
+    summary of this workload (profiles/r*_<PROFILE_TAG>_traffic.json, made by
+    scripts/make_profile_summary.py): HBM bytes per launch, MFMA utilisation
+    (SQ_VALU_MFMA_BUSY_CYCLES over the SIMD cycles of GRBM_GUI_ACTIVE) and the
+    clock the launch ran at."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")),
-                   key=lambda f: (os.path.basename(f).startswith("r2"), os.path.getmtime(f)))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{PROFILE_TAG}_traffic.json")),
+                   key=lambda f: os.path.basename(f))
     for f in reversed(files):
         d = json.load(open(f))
         for key, v in d.items():
@@ -334,6 +342,8 @@ def main():
     hubert = args.arch == HUBERT_ARCH
     simam = args.arch.startswith("SimAM")
     resnet_like = args.arch.startswith("ResNet") or simam
+    global PROFILE_TAG
+    PROFILE_TAG = {"ECAPA_TDNN_c1024": "c2", "ResNet293": "c3", HUBERT_ARCH: "c4"}.get(args.arch, "none")
     # C4 per GPU: 256 utterances like C2 (fc2 / out_proj have 3 column tiles of 256:
     # 64 utterances fill 189 of the 256 CUs; 256 fill 2.9 rounds; +12.5 % over 64)
     B = args.batch or (128 if resnet_like else 256)
