@@ -166,6 +166,30 @@ def resnet_1x1_bytes_per_utt(arch: str, F: int, T: int, m: int = 32) -> float:
     return total
 
 
+def resnet_model_bytes_per_utt(arch: str, F: int, T: int, m: int = 32) -> float:
+    """Algorithmic HBM bytes of one whole bottleneck-ResNet forward (resnet.py:110-260):
+    every conv's fp32 input read once and output written once (the stem, the 1x1
+    convs with conv3's residual read, the 3x3 convs, the projection shortcuts), plus
+    the pooling read of the last activations; weights excluded."""
+    kind, nblocks = RESNET_ARCHS[arch]
+    if kind != "bottleneck":
+        return 0.0
+    total = 4.0 * F * T * (1 + m)  # stem 3x3: 1 -> m channels
+    cin, fi, ti = m, F, T
+    for li, n in enumerate(nblocks):
+        p = m << li
+        for bi in range(n):
+            s = 2 if (li > 0 and bi == 0) else 1
+            fo, to = (fi - 1) // s + 1, (ti - 1) // s + 1
+            total += 4.0 * fi * ti * (cin + p)             # conv1
+            total += 4.0 * (fi * ti * p + fo * to * p)     # conv2 (3x3, stride s)
+            total += 4.0 * fo * to * (p + 4 * p + 4 * p)   # conv3 + residual
+            if s != 1 or cin != 4 * p:
+                total += 4.0 * fo * to * (cin + 4 * p)     # projection shortcut
+            cin, fi, ti = 4 * p, fo, to
+    return total + 4.0 * fi * ti * cin                     # statistics pooling read
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -518,6 +542,13 @@ def main():
                     "algorithmic_bytes": byts, "launches_per_step": kr["launches_per_step"],
                     "ms_per_step": kr["ms_per_step"],
                     "concurrent_streams": streams}
+            # whole-model byte roofline: every conv's algorithmic bytes of a step over the
+            # measured step time (fbank included), independent of how launches overlap
+            mb = resnet_model_bytes_per_utt(args.arch, 80, T) * B
+            if mb and el > 0:
+                mg = mb / (el / args.steps) / 1e9
+                roof["model"] = {"algorithmic_bytes_per_step": mb, "achieved": round(mg, 1),
+                                 "frac": round(mg / HBM_PEAK_GBPS, 4)}
             if streams > 1:
                 roof["note"] = ("launch durations measured beside the other utterance range's kernels "
                                 "(option streams); --opt streams=1 gives the standalone rate")
