@@ -147,6 +147,8 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *                  W2 in registers and a deeper ring (default; all three bit-identical);
  *                  0 = linear2 GEMM + separate pooling kernel
  *   "attn_lds"     HuBERT: 1 = K / V staged once per 256-key block in LDS (default)
+ *   "conv3x3_img"  ResNet bottleneck: 1 = stride-1 3x3 convs with 32 / 64 channels from an LDS
+ *                  image of the input patch (default), 0 = implicit GEMM (bit-identical)
  *   "in_planes"    SimAM-ResNet, before the weights: 32 or 64
  *   "layer"        HuBERT front end only, before finalize: -1 = weighted sum of all
  *                  hidden states (default), k = hidden state k alone (s3prl.py:84-87) */

@@ -1,0 +1,56 @@
+"""GPU: the LDS-image 3x3 conv (conv3x3_img.hip, ResNet bottleneck conv2 with
+32 / 64 channels, stride 1; resnet.py:72-107) against the implicit GEMM it
+replaces (option conv3x3_img=0) and the oracle.
+
+Both kernels add the same bf16 hi/lo products in the same k order (tap-major,
+conv_gemm_x3's 2-D order) with the same epilogue, so the embeddings must be
+bit-identical; shapes cover partial time tiles (T not a multiple of 64 / 32),
+the stride-2 first block of stage 2 (implicit GEMM) next to its stride-1 blocks,
+and the 2-GiB chunking of a larger batch."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import models_ref
+from wespeaker_hubert_amd.synthetic import synth_feats, synth_state_dict
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _pair(arch, seed):
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    ms, sd = [], None
+    for on in (1, 0):
+        m = HipSpeakerModel(arch, feat_dim=80, embed_dim=256)
+        m.set_option("conv3x3_img", on)
+        if sd is None:
+            sd = synth_state_dict(seed, m.state_dict_layout(), residual_tame=True)
+        m.load_state_dict(sd)
+        ms.append(m.to(DEV))
+    return ms[0], ms[1], sd
+
+
+@pytest.mark.parametrize("arch,B,T", [("ResNet50", 3, 100), ("ResNet50", 2, 37), ("ResNet101", 1, 200),
+                                      ("ResNet293", 2, 64)])
+def test_conv3x3_img_equals_implicit_gemm_and_oracle(arch, B, T):
+    img, gemm, sd = _pair(arch, 31)
+    x = torch.from_numpy(synth_feats(9, B, T, 80)).to(DEV)
+    a = img.embed(x).cpu().numpy()
+    b = gemm.embed(x).cpu().numpy()
+    assert np.all(np.isfinite(a))
+    assert np.array_equal(a, b), np.abs(a - b).max()
+    rows = list(range(min(B, 2)))
+    with torch.no_grad():
+        _, ref = models_ref.forward(arch, x[rows].cpu(), {k: torch.from_numpy(v) for k, v in sd.items()})
+    assert np.abs(a[rows] - ref.numpy()).max() < 1e-4
+
+
+def test_conv3x3_img_batch_rows_equal_batch_of_one():
+    img, _, _ = _pair("ResNet50", 32)
+    x = torch.from_numpy(synth_feats(10, 6, 150, 80)).to(DEV)
+    full = img.embed(x).cpu().numpy()
+    for i in (0, 3, 5):
+        one = img.embed(x[i:i + 1]).cpu().numpy()[0]
+        assert np.array_equal(full[i], one)

@@ -234,6 +234,9 @@ void Model::set_option(const std::string& key, int value) {
   } else if (key == "astp_fused") {
     WSP_CHECK(value >= 0 && value <= 3, "astp_fused must be 0 (unfused) or 1..3 (fused kernel variant)");
     impl->astp_fused_on = value;
+  } else if (key == "conv3x3_img") {
+    WSP_CHECK(value == 0 || value == 1, "conv3x3_img must be 0 or 1");
+    impl->conv3x3_img_on = value;
   } else if (key == "streams") {
     WSP_CHECK(value >= 1 && value <= 8, "streams must be 1..8");
     impl->streams = value;
@@ -258,6 +261,7 @@ int Model::get_option(const std::string& key) const {
   if (key == "astp_fused") return m.astp_fused_on;
   if (key == "res2_variant") return m.res2_variant;
   if (key == "x3_variant") return m.x3_variant;
+  if (key == "conv3x3_img") return m.conv3x3_img_on;
   throw InvalidArg{"unknown option " + key};
 }
 

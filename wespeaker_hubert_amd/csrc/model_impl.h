@@ -18,6 +18,7 @@
 #include "res2_chain.h"
 #include "gemm_dma.h"
 #include "astp_fused.h"
+#include "conv3x3_img.h"
 
 namespace wsp {
 
@@ -54,6 +55,7 @@ struct ConvW {
   float* scale = nullptr;
   float* shift = nullptr;
   int N = 0, cin = 0, taps = 1, K = 0, Kp = 0;
+  void* frag = nullptr;  // 3x3, N = cin = 32 / 64: MFMA B-fragment order for conv3x3_img.hip
 };
 
 struct LinW {  // small_linear weights, k-major
@@ -140,6 +142,7 @@ struct Model::Impl {
     float *r2b = nullptr, *r2s = nullptr, *r2t = nullptr;
   } blk[3];
   int res2_fused = 1;  // 0: the 7-launch GEMM chain (A/B option "res2_fused")
+  int conv3x3_img_on = 1;  // ResNet stride-1 3x3 convs with 32 / 64 channels on conv3x3_img.hip (option "conv3x3_img")
   int res2_variant = 0;  // res2_chain.hip kernel variant (option "res2_variant")
   ConvW conv, pool1, pool2;
   void* pool2_frag = nullptr;  // pool.linear2 in MFMA B-fragment order for astp_fused.hip
@@ -437,7 +440,16 @@ struct Model::Impl {
       for (int k = 0; k < cin * taps; ++k) w[(size_t)n * cin * taps + k] = (float)(w[(size_t)n * cin * taps + k] * sc[n]);
     std::vector<float> b(N);
     for (int n = 0; n < N; ++n) b[n] = (float)sh[n];
-    return pack_conv(w, N, cin, taps, b.data(), "");
+    ConvW cw = pack_conv(w, N, cin, taps, b.data(), "");
+    if (taps == 9 && N == cin && conv3x3_img_supported(cin)) {
+      // the same k = tap * cin + c order as the implicit GEMM's packed image
+      std::vector<float> wk((size_t)N * 9 * cin);
+      for (int n = 0; n < N; ++n)
+        for (int c = 0; c < cin; ++c)
+          for (int j = 0; j < 9; ++j) wk[(size_t)n * 9 * cin + j * cin + c] = w[((size_t)n * cin + c) * 9 + j];
+      cw.frag = pack_frag(wk, N, 9 * cin);
+    }
+    return cw;
   }
 
   void finalize_resnet() {
@@ -618,7 +630,14 @@ struct Model::Impl {
         }
         if (bottleneck) {
           gemm1x1(kC1[li], rb.c1, x, Y1, nb * Fi * Ti, kActRelu, nullptr, s);
-          gemm2d(kK3[li], rb.c2, Y1, rb.planes, Y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
+          if (rb.stride == 1 && rb.c2.frag && conv3x3_img_on) {
+            const Conv3x3Args a{Y1, Y2, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift};
+            run(kK3[li], 2.0 * nb * Fi * Ti * rb.c2.N * rb.c2.K, s,
+                [&] { launch_conv3x3_img(a, rb.planes, s); });
+          } else {
+            gemm2d(kK3[li], rb.c2, Y1, rb.planes, Y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0,
+                   s);
+          }
           gemm1x1(kC3[li], rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
         } else {
           gemm2d(kK3[li], rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
