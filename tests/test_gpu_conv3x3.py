@@ -6,7 +6,8 @@ Both kernels add the same bf16 hi/lo products in the same k order (tap-major,
 conv_gemm_x3's 2-D order) with the same epilogue, so the embeddings must be
 bit-identical; shapes cover partial time tiles (T not a multiple of 64 / 32),
 the stride-2 first block of stage 2 (implicit GEMM) next to its stride-1 blocks,
-and the 2-GiB chunking of a larger batch."""
+basic blocks (ResNet18/34: both 3x3 convs, the second with the residual in its
+epilogue), and batch independence."""
 import numpy as np
 import pytest
 import torch
@@ -33,7 +34,7 @@ def _pair(arch, seed):
 
 
 @pytest.mark.parametrize("arch,B,T", [("ResNet50", 3, 100), ("ResNet50", 2, 37), ("ResNet101", 1, 200),
-                                      ("ResNet293", 2, 64)])
+                                      ("ResNet293", 2, 64), ("ResNet34", 3, 77), ("ResNet18", 2, 9)])
 def test_conv3x3_img_equals_implicit_gemm_and_oracle(arch, B, T):
     img, gemm, sd = _pair(arch, 31)
     x = torch.from_numpy(synth_feats(9, B, T, 80)).to(DEV)

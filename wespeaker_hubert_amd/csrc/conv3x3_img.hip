@@ -1,6 +1,7 @@
 // Stride-1 3x3 conv with C = 32 / 64 channels (the ResNet bottleneck conv2 of
-// stages 1-2, resnet.py:72-107) on bf16x3 MFMA from an LDS image of the input
-// patch.
+// stages 1-2, resnet.py:72-107, and the basic-block convs of ResNet18/34,
+// resnet.py:44-69, with the residual in the epilogue) on bf16x3 MFMA from an LDS
+// image of the input patch.
 //
 // The implicit GEMM (conv_gemm_x3 with ALoader2D) stages, for every 32-wide
 // k-tile, the tile's rows of ONE tap from global memory: each input position is
@@ -45,7 +46,7 @@ struct Img {
   __device__ __forceinline__ static int addr(int r, int ch) { return r * RB + ((ch ^ sw(r)) << 4); }
 };
 
-template <int C, int FB, int TB, int MINB>
+template <int C, int FB, int TB, int MINB, bool RES>
 __global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Conv3x3Args p) {
   using G = Img<C, FB, TB>;
   constexpr int TN = G::TN, PT = G::PT;
@@ -152,8 +153,9 @@ __global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Con
     wload(g + 3, b1h, b1l);
   }
 
-  // ---- epilogue (conv_gemm_x3's: y = relu(acc + bias) * scale + shift)
+  // ---- epilogue (conv_gemm_x3's: y = relu(acc + bias (+ res)) * scale + shift)
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out + ubase);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc((RES ? p.res : p.out) + ubase);
   const int f = f0 + lf;
   const int tw = t0 + lt0 + 4 * h;  // time of register 0
 #pragma unroll
@@ -162,10 +164,20 @@ __global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Con
     const float bv = p.bias ? p.bias[col] : 0.f;
     const float sc = p.scale ? p.scale[col] : 1.f;
     const float sh = p.scale ? p.shift[col] : 0.f;
+    float rv[16];
+    if constexpr (RES) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int t = tw + (r & 3) + 8 * (r >> 2);
+        rv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rr, f < p.F && t < p.T ? ((f * p.T + t) * C + col) * 4 : kOOB, 0, 0));
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int t = tw + (r & 3) + 8 * (r >> 2);
       float y = acc[j][r] + bv;
+      if constexpr (RES) y += rv[r];
       y = fmaxf(y, 0.f);
       y = y * sc + sh;
       const bool ok = f < p.F && t < p.T;
@@ -179,7 +191,10 @@ template <int C, int FB, int TB, int MINB>
 void launch_k(const Conv3x3Args& p, hipStream_t s) {
   using G = Img<C, FB, TB>;
   const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + TB - 1) / TB);
-  hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
+  if (p.res)
+    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB, true>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
+  else
+    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB, false>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
 }
 
 }  // namespace

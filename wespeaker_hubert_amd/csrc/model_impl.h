@@ -640,9 +640,19 @@ struct Model::Impl {
           }
           gemm1x1(kC3[li], rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
         } else {
-          gemm2d(kK3[li], rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
-          gemm2d(kK3[li], rb.c2, Y1, rb.planes, o, rb.out_planes, nb, Fo, To, 3, 1, 1, kActRelu, res,
-                 rb.out_planes, s);
+          if (rb.stride == 1 && rb.c1.frag && conv3x3_img_on) {
+            const Conv3x3Args a{x, Y1, nb, Fi, Ti, rb.c1.frag, rb.c1.bias, rb.c1.scale, rb.c1.shift};
+            run(kK3[li], 2.0 * nb * Fi * Ti * rb.c1.N * rb.c1.K, s, [&] { launch_conv3x3_img(a, rb.planes, s); });
+          } else {
+            gemm2d(kK3[li], rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
+          }
+          if (rb.c2.frag && conv3x3_img_on && rb.out_planes == rb.planes) {
+            const Conv3x3Args a{Y1, o, nb, Fo, To, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, res};
+            run(kK3[li], 2.0 * nb * Fo * To * rb.c2.N * rb.c2.K, s, [&] { launch_conv3x3_img(a, rb.planes, s); });
+          } else {
+            gemm2d(kK3[li], rb.c2, Y1, rb.planes, o, rb.out_planes, nb, Fo, To, 3, 1, 1, kActRelu, res,
+                   rb.out_planes, s);
+          }
         }
         std::swap(x, o);
         Fi = Fo;
