@@ -34,7 +34,8 @@ def _pair(arch, seed):
 
 
 @pytest.mark.parametrize("arch,B,T", [("ResNet50", 3, 100), ("ResNet50", 2, 37), ("ResNet101", 1, 200),
-                                      ("ResNet293", 2, 64), ("ResNet34", 3, 77), ("ResNet18", 2, 9)])
+                                      ("ResNet293", 2, 64), ("ResNet34", 3, 77), ("ResNet18", 2, 9),
+                                      ("SimAM_ResNet34_ASP", 2, 64)])
 def test_conv3x3_img_equals_implicit_gemm_and_oracle(arch, B, T):
     img, gemm, sd = _pair(arch, 31)
     x = torch.from_numpy(synth_feats(9, B, T, 80)).to(DEV)

@@ -20,6 +20,7 @@ struct Conv3x3Args {
   const float* scale;
   const float* shift;
   const float* res = nullptr;  // optional residual [B][F][T][C], added before the ReLU (basic blocks)
+  int relu = 1;                // 0: no activation (SimAM-ResNet conv2, whose BN output feeds SimAM)
 };
 bool conv3x3_img_supported(int C);
 void launch_conv3x3_img(const Conv3x3Args& p, int C, hipStream_t s);

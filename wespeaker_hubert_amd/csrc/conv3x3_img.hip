@@ -1,7 +1,8 @@
 // Stride-1 3x3 conv with C = 32 / 64 channels (the ResNet bottleneck conv2 of
 // stages 1-2, resnet.py:72-107, and the basic-block convs of ResNet18/34,
-// resnet.py:44-69, with the residual in the epilogue) on bf16x3 MFMA from an LDS
-// image of the input patch.
+// resnet.py:44-69, with the residual in the epilogue, and the SimAM-ResNet
+// basic-block convs, samresnet.py:20-60) on bf16x3 MFMA from an LDS image of the
+// input patch.
 //
 // The implicit GEMM (conv_gemm_x3 with ALoader2D) stages, for every 32-wide
 // k-tile, the tile's rows of ONE tap from global memory: each input position is
@@ -46,7 +47,7 @@ struct Img {
   __device__ __forceinline__ static int addr(int r, int ch) { return r * RB + ((ch ^ sw(r)) << 4); }
 };
 
-template <int C, int FB, int TB, int MINB, bool RES>
+template <int C, int FB, int TB, int MINB, bool RES, bool RELU>
 __global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Conv3x3Args p) {
   using G = Img<C, FB, TB>;
   constexpr int TN = G::TN, PT = G::PT;
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Con
     wload(g + 3, b1h, b1l);
   }
 
-  // ---- epilogue (conv_gemm_x3's: y = relu(acc + bias (+ res)) * scale + shift)
+  // ---- epilogue (conv_gemm_x3's: y = act(acc + bias (+ res)) * scale + shift)
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out + ubase);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc((RES ? p.res : p.out) + ubase);
   const int f = f0 + lf;
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Con
       const int t = tw + (r & 3) + 8 * (r >> 2);
       float y = acc[j][r] + bv;
       if constexpr (RES) y += rv[r];
-      y = fmaxf(y, 0.f);
+      if constexpr (RELU) y = fmaxf(y, 0.f);
       y = y * sc + sh;
       const bool ok = f < p.F && t < p.T;
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro,
@@ -192,9 +193,11 @@ void launch_k(const Conv3x3Args& p, hipStream_t s) {
   using G = Img<C, FB, TB>;
   const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + TB - 1) / TB);
   if (p.res)
-    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB, true>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
+    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB, true, true>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
+  else if (p.relu)
+    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB, false, true>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
   else
-    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB, false>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
+    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB, false, false>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
 }
 
 }  // namespace
@@ -204,6 +207,7 @@ bool conv3x3_img_supported(int C) { return C == 32 || C == 64; }
 void launch_conv3x3_img(const Conv3x3Args& p, int C, hipStream_t s) {
   WSP_CHECK(conv3x3_img_supported(C), "conv3x3_img: channels must be 32 or 64");
   WSP_CHECK(p.B > 0 && p.F > 0 && p.T > 0 && p.x && p.out && p.w, "conv3x3_img: bad arguments");
+  WSP_CHECK(p.relu || !p.res, "conv3x3_img: a residual comes with the ReLU");
   // buffer offsets are per utterance (descriptors based at its first element)
   WSP_CHECK((long long)p.F * p.T * C * 4 < (long long)kOOB, "conv3x3_img: utterance exceeds 2 GiB");
   if (C == 32)

@@ -824,8 +824,18 @@ struct Model::Impl {
           gemm2d("shortcut", rb.sc, x, Ci, SC, rb.planes, nb, Fi, Ti, 1, rb.stride, 0, kActNone, nullptr, 0, s);
           res = SC;
         }
-        gemm2d("res_conv3x3", rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
-        gemm2d("res_conv3x3", rb.c2, Y1, rb.planes, Z, rb.planes, nb, Fo, To, 3, 1, 1, kActNone, nullptr, 0, s);
+        if (rb.stride == 1 && rb.c1.frag && conv3x3_img_on) {
+          const Conv3x3Args a{x, Y1, nb, Fi, Ti, rb.c1.frag, rb.c1.bias, rb.c1.scale, rb.c1.shift};
+          run("res_conv3x3", 2.0 * nb * Fi * Ti * rb.c1.N * rb.c1.K, s, [&] { launch_conv3x3_img(a, rb.planes, s); });
+        } else {
+          gemm2d("res_conv3x3", rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
+        }
+        if (rb.c2.frag && conv3x3_img_on) {
+          const Conv3x3Args a{Y1, Z, nb, Fo, To, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, nullptr, 0};
+          run("res_conv3x3", 2.0 * nb * Fo * To * rb.c2.N * rb.c2.K, s, [&] { launch_conv3x3_img(a, rb.planes, s); });
+        } else {
+          gemm2d("res_conv3x3", rb.c2, Y1, rb.planes, Z, rb.planes, nb, Fo, To, 3, 1, 1, kActNone, nullptr, 0, s);
+        }
         run("simam", 0, s, [&] { launch_simam(Z, res, o, nb, Fo * To, rb.planes, part, coef, s); });
         std::swap(x, o);
         Fi = Fo;
