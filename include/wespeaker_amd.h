@@ -147,8 +147,13 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *                  W2 in registers and a deeper ring (default; all three bit-identical);
  *                  0 = linear2 GEMM + separate pooling kernel
  *   "attn_lds"     HuBERT: 1 = K / V staged once per 256-key block in LDS (default)
- *   "conv3x3_img"  ResNet bottleneck: 1 = stride-1 3x3 convs with 32 / 64 channels from an LDS
- *                  image of the input patch (default), 0 = implicit GEMM (bit-identical)
+ *   "conv3x3_img"  ResNet / SimAM-ResNet stride-1 3x3 convs from an LDS image of the input
+ *                  patch (bit-identical to the implicit GEMM): 1 = 32 / 64 channels, 2 = also
+ *                  128 channels, 4 x 32 positions x 4 column tiles per wave (default), 3 = also
+ *                  128 channels, 8 waves x 2 column tiles; 0 = implicit GEMM throughout
+ *   "cat_gate"     ECAPA-TDNN: 1 = conv_cat on [out2, out3, out4 - out3] with weights
+ *                  [W_a, W_b + W_c, W_c], so the last SE block stores only its gated branch
+ *                  (default; equal to 0 up to rounding, ~1e-6), 0 = conv_cat on [out2, out3, out4]
  *   "in_planes"    SimAM-ResNet, before the weights: 32 or 64
  *   "layer"        HuBERT front end only, before finalize: -1 = weighted sum of all
  *                  hidden states (default), k = hidden state k alone (s3prl.py:84-87) */

@@ -1,5 +1,5 @@
 """GPU: the LDS-image 3x3 conv (conv3x3_img.hip, ResNet bottleneck conv2 with
-32 / 64 channels, stride 1; resnet.py:72-107) against the implicit GEMM it
+32 / 64 / 128 channels, stride 1; resnet.py:72-107) against the implicit GEMM it
 replaces (option conv3x3_img=0) and the oracle.
 
 Both kernels add the same bf16 hi/lo products in the same k order (tap-major,
@@ -20,10 +20,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-def _pair(arch, seed):
+def _pair(arch, seed, img=1):
     from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
     ms, sd = [], None
-    for on in (1, 0):
+    for on in (img, 0):
         m = HipSpeakerModel(arch, feat_dim=80, embed_dim=256)
         m.set_option("conv3x3_img", on)
         if sd is None:
@@ -33,11 +33,16 @@ def _pair(arch, seed):
     return ms[0], ms[1], sd
 
 
-@pytest.mark.parametrize("arch,B,T", [("ResNet50", 3, 100), ("ResNet50", 2, 37), ("ResNet101", 1, 200),
-                                      ("ResNet293", 2, 64), ("ResNet34", 3, 77), ("ResNet18", 2, 9),
-                                      ("SimAM_ResNet34_ASP", 2, 64)])
-def test_conv3x3_img_equals_implicit_gemm_and_oracle(arch, B, T):
-    img, gemm, sd = _pair(arch, 31)
+CASES = [("ResNet50", 3, 100), ("ResNet50", 2, 37), ("ResNet101", 1, 200), ("ResNet293", 2, 64),
+         ("ResNet34", 3, 77), ("ResNet18", 2, 9), ("SimAM_ResNet34_ASP", 2, 64)]
+
+
+# option conv3x3_img: 1 = 32 / 64 channels on the image kernel, 2 / 3 = also 128 channels
+# (stage 3 of the ResNets, stage 2 of SimAM-ResNet34; 4 x 32 and 2 x 32 position tiles)
+@pytest.mark.parametrize("img", [1, 2, 3])
+@pytest.mark.parametrize("arch,B,T", CASES)
+def test_conv3x3_img_equals_implicit_gemm_and_oracle(arch, B, T, img):
+    img, gemm, sd = _pair(arch, 31, img)
     x = torch.from_numpy(synth_feats(9, B, T, 80)).to(DEV)
     a = img.embed(x).cpu().numpy()
     b = gemm.embed(x).cpu().numpy()
@@ -49,8 +54,9 @@ def test_conv3x3_img_equals_implicit_gemm_and_oracle(arch, B, T):
     assert np.abs(a[rows] - ref.numpy()).max() < 1e-4
 
 
-def test_conv3x3_img_batch_rows_equal_batch_of_one():
-    img, _, _ = _pair("ResNet50", 32)
+@pytest.mark.parametrize("img", [1, 2])
+def test_conv3x3_img_batch_rows_equal_batch_of_one(img):
+    img, _, _ = _pair("ResNet50", 32, img)
     x = torch.from_numpy(synth_feats(10, 6, 150, 80)).to(DEV)
     full = img.embed(x).cpu().numpy()
     for i in (0, 3, 5):

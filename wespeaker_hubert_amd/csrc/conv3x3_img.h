@@ -21,6 +21,7 @@ struct Conv3x3Args {
   const float* shift;
   const float* res = nullptr;  // optional residual [B][F][T][C], added before the ReLU (basic blocks)
   int relu = 1;                // 0: no activation (SimAM-ResNet conv2, whose BN output feeds SimAM)
+  int variant = 0;             // C = 128 tile: 3 = 2 x 32 positions (two blocks per CU), else 4 x 32
 };
 bool conv3x3_img_supported(int C);
 void launch_conv3x3_img(const Conv3x3Args& p, int C, hipStream_t s);

@@ -1,5 +1,5 @@
-// Stride-1 3x3 conv with C = 32 / 64 channels (the ResNet bottleneck conv2 of
-// stages 1-2, resnet.py:72-107, and the basic-block convs of ResNet18/34,
+// Stride-1 3x3 conv with C = 32 / 64 / 128 channels (the ResNet bottleneck conv2 of
+// stages 1-3, resnet.py:72-107, and the basic-block convs of ResNet18/34,
 // resnet.py:44-69, with the residual in the epilogue, and the SimAM-ResNet
 // basic-block convs, samresnet.py:20-60) on bf16x3 MFMA from an LDS image of the
 // input patch.
@@ -16,6 +16,10 @@
 // L1 / L2, two k-steps ahead in registers (the res2_chain.hip scheme), so the
 // k-loop has no barrier.  k order, MFMA order and epilogue are conv_gemm_x3's:
 // the results are bit-identical to the implicit GEMM.
+// C = 128 (102 KB image of a 4 x 32 tile, one block per CU): each wave owns one
+// 32-position time run and all 128 channels (4 column tiles), or with WN = 2 half
+// of them (8 waves; option conv3x3_img 3).  r2: ResNet293 stage-3 3x3 21.2 ->
+// 18.4 ms/step (one stream), C3 1 260 -> 1 280 emb/s, ResNet34 10 740 -> 11 030.
 #include "conv3x3_img.h"
 #include "gemm_common.h"
 
@@ -26,16 +30,17 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-template <int C, int FB, int TB>
+template <int C, int FB, int TB, int WN = 1>
 struct Img {
   static constexpr int PT = TB + 2;
   static constexpr int IR = (FB + 2) * PT;  // patch positions
   static constexpr int RB = 2 * C;          // bytes per image row and plane
   static constexpr int PLANE = IR * RB;
   static constexpr int LDS = 2 * PLANE;
-  static constexpr int NW = FB * TB / 32;   // waves: 32 positions (one time run) each
+  static constexpr int NW = FB * TB / 32 * WN;  // waves: 32 positions (one time run) x C / WN channels each
   static constexpr int NT = NW * 64;
-  static constexpr int TN = C / 32;         // 32-channel column tiles per wave
+  static constexpr int CT = C / 32;         // 32-channel column tiles
+  static constexpr int TN = CT / WN;        // column tiles per wave
   static constexpr int KC = C / 16;         // k-steps per tap
   static constexpr int KS = 9 * KC;         // k-steps
   static constexpr int C4 = C / 4;
@@ -43,13 +48,15 @@ struct Img {
   static_assert(TB % 32 == 0 && KS % 2 == 0, "conv3x3_img tile");
   // 16-B chunk ch of row r at slot ch ^ sw(r): the 16 rows of a ds_read_b128 lane
   // group (16 distinct rows mod 16) hit 16 distinct slots of the 256-B bank row
-  __device__ __forceinline__ static int sw(int r) { return C == 32 ? ((r >> 2) & 3) : ((r >> 1) & 7); }
+  __device__ __forceinline__ static int sw(int r) {
+    return C == 32 ? ((r >> 2) & 3) : C == 64 ? ((r >> 1) & 7) : (r & 15);
+  }
   __device__ __forceinline__ static int addr(int r, int ch) { return r * RB + ((ch ^ sw(r)) << 4); }
 };
 
-template <int C, int FB, int TB, int MINB, bool RES, bool RELU>
-__global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Conv3x3Args p) {
-  using G = Img<C, FB, TB>;
+template <int C, int FB, int TB, int WN, int MINB, bool RES, bool RELU>
+__global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void conv3x3_img_kernel(const Conv3x3Args p) {
+  using G = Img<C, FB, TB, WN>;
   constexpr int TN = G::TN, PT = G::PT;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* xhi = smem;
@@ -104,8 +111,9 @@ __global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Con
 
   // this lane's output position: patch-local (lf, lt); tap (kf, kt) reads image row
   // (lf + kf) * PT + lt + kt
-  const int lf = wave / (TB / 32);
-  const int lt0 = (wave % (TB / 32)) * 32;
+  const int pr = wave / WN, wn = wave - pr * WN;  // position run, column group
+  const int lf = pr / (TB / 32);
+  const int lt0 = (pr % (TB / 32)) * 32;
   const int row0 = lf * PT + lt0 + r32;
 
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w);
@@ -113,9 +121,9 @@ __global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Con
     const bool ok = g < G::KS;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int o = ((g * 2 * TN + j) * 64 + lane) * 16;
+      const int o = ((g * 2 * G::CT + wn * TN + j) * 64 + lane) * 16;
       bh[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? o : kOOB, 0, 0));
-      bl[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? o + TN * 1024 : kOOB, 0, 0));
+      bl[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? o + G::CT * 1024 : kOOB, 0, 0));
     }
   };
   auto read_a = [&](int g, bf16x8& ah, bf16x8& al) {
@@ -161,7 +169,7 @@ __global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Con
   const int tw = t0 + lt0 + 4 * h;  // time of register 0
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col = j * 32 + r32;
+    const int col = (wn * TN + j) * 32 + r32;
     const float bv = p.bias ? p.bias[col] : 0.f;
     const float sc = p.scale ? p.scale[col] : 1.f;
     const float sh = p.scale ? p.shift[col] : 0.f;
@@ -188,32 +196,36 @@ __global__ __launch_bounds__(FB* TB * 2, MINB) void conv3x3_img_kernel(const Con
   }
 }
 
-template <int C, int FB, int TB, int MINB>
+template <int C, int FB, int TB, int MINB, int WN = 1>
 void launch_k(const Conv3x3Args& p, hipStream_t s) {
-  using G = Img<C, FB, TB>;
+  using G = Img<C, FB, TB, WN>;
   const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + TB - 1) / TB);
   if (p.res)
-    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB, true, true>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
+    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, WN, MINB, true, true>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
   else if (p.relu)
-    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB, false, true>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
+    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, WN, MINB, false, true>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
   else
-    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, MINB, false, false>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
+    hipLaunchKernelGGL((conv3x3_img_kernel<C, FB, TB, WN, MINB, false, false>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
 }
 
 }  // namespace
 
-bool conv3x3_img_supported(int C) { return C == 32 || C == 64; }
+bool conv3x3_img_supported(int C) { return C == 32 || C == 64 || C == 128; }
 
 void launch_conv3x3_img(const Conv3x3Args& p, int C, hipStream_t s) {
-  WSP_CHECK(conv3x3_img_supported(C), "conv3x3_img: channels must be 32 or 64");
+  WSP_CHECK(conv3x3_img_supported(C), "conv3x3_img: channels must be 32, 64 or 128");
   WSP_CHECK(p.B > 0 && p.F > 0 && p.T > 0 && p.x && p.out && p.w, "conv3x3_img: bad arguments");
   WSP_CHECK(p.relu || !p.res, "conv3x3_img: a residual comes with the ReLU");
   // buffer offsets are per utterance (descriptors based at its first element)
   WSP_CHECK((long long)p.F * p.T * C * 4 < (long long)kOOB, "conv3x3_img: utterance exceeds 2 GiB");
   if (C == 32)
     launch_k<32, 4, 64, 3>(p, s);  // 256 positions, 8 waves, 50 KB image: 3 blocks / CU
-  else
+  else if (C == 64)
     launch_k<64, 4, 32, 3>(p, s);  // 128 positions, 4 waves x 2 column tiles, 51 KB image
+  else if (p.variant == 3)
+    launch_k<128, 4, 32, 1, 2>(p, s);  // 128 positions, 8 waves x 2 column tiles, 102 KB image
+  else
+    launch_k<128, 4, 32, 1>(p, s);  // 128 positions, 4 waves x 4 column tiles, 102 KB image
   WSP_HIP(hipGetLastError());
 }
 

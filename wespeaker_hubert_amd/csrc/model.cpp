@@ -225,6 +225,9 @@ void Model::set_option(const std::string& key, int value) {
     for (const auto& p : impl->params) WSP_CHECK(!p.set, "option 'in_planes' must be set before the weights");
     impl->m_ch = value;
     impl->build_simam_params();
+  } else if (key == "cat_gate") {
+    WSP_CHECK(value == 0 || value == 1, "cat_gate must be 0 or 1");
+    impl->cat_gate = value;
   } else if (key == "res2_fused") {
     WSP_CHECK(value == 0 || value == 1, "res2_fused must be 0 or 1");
     impl->res2_fused = value;
@@ -235,7 +238,7 @@ void Model::set_option(const std::string& key, int value) {
     WSP_CHECK(value >= 0 && value <= 3, "astp_fused must be 0 (unfused) or 1..3 (fused kernel variant)");
     impl->astp_fused_on = value;
   } else if (key == "conv3x3_img") {
-    WSP_CHECK(value == 0 || value == 1, "conv3x3_img must be 0 or 1");
+    WSP_CHECK(value >= 0 && value <= 3, "conv3x3_img must be 0 (off), 1 (32 / 64 channels) or 2 / 3 (also 128)");
     impl->conv3x3_img_on = value;
   } else if (key == "streams") {
     WSP_CHECK(value >= 1 && value <= 8, "streams must be 1..8");
@@ -257,6 +260,7 @@ int Model::get_option(const std::string& key) const {
   if (key == "layer") return m.h_layer_sel;
   if (key == "in_planes") return m.m_ch;
   if (key == "res2_fused") return m.res2_fused;
+  if (key == "cat_gate") return m.cat_gate;
   if (key == "attn_lds") return m.attn_lds;
   if (key == "astp_fused") return m.astp_fused_on;
   if (key == "res2_variant") return m.res2_variant;

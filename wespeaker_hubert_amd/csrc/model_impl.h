@@ -142,9 +142,17 @@ struct Model::Impl {
     float *r2b = nullptr, *r2s = nullptr, *r2t = nullptr;
   } blk[3];
   int res2_fused = 1;  // 0: the 7-launch GEMM chain (A/B option "res2_fused")
-  int conv3x3_img_on = 1;  // ResNet stride-1 3x3 convs with 32 / 64 channels on conv3x3_img.hip (option "conv3x3_img")
+  // ResNet stride-1 3x3 convs on conv3x3_img.hip (option "conv3x3_img"): 0 = off (implicit GEMM),
+  // 1 = 32 / 64 channels, 2 = also 128 channels (4 x 32 tile), 3 = also 128 (2 x 32 tile)
+  int conv3x3_img_on = 2;
+  bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
   int res2_variant = 0;  // res2_chain.hip kernel variant (option "res2_variant")
   ConvW conv, pool1, pool2;
+  // conv_cat on [out2, out3, g4 * h3_4]: out4 = out3 + g4 * h3_4, so W . [out2; out3; out4]
+  // = W_a out2 + (W_b + W_c) out3 + W_c (g4 * h3_4) — the last SE block's residual pass
+  // writes only g4 * h3_4 (no residual read) (option "cat_gate", default on)
+  ConvW conv_g;
+  int cat_gate = 1;
   void* pool2_frag = nullptr;  // pool.linear2 in MFMA B-fragment order for astp_fused.hip
   // 0: linear2 GEMM + separate pooling kernel; 1..3: astp_fused.hip variant (option "astp_fused";
   // 3 = 256 channels per block, att chunks two ahead in an LDS-DMA ring, W2 in VGPRs: C2 0.465 -> 0.31 ms)
@@ -630,8 +638,8 @@ struct Model::Impl {
         }
         if (bottleneck) {
           gemm1x1(kC1[li], rb.c1, x, Y1, nb * Fi * Ti, kActRelu, nullptr, s);
-          if (rb.stride == 1 && rb.c2.frag && conv3x3_img_on) {
-            const Conv3x3Args a{Y1, Y2, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift};
+          if (rb.stride == 1 && img_ok(rb.c2, rb.planes)) {
+            const Conv3x3Args a{Y1, Y2, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, nullptr, 1, conv3x3_img_on};
             run(kK3[li], 2.0 * nb * Fi * Ti * rb.c2.N * rb.c2.K, s,
                 [&] { launch_conv3x3_img(a, rb.planes, s); });
           } else {
@@ -640,14 +648,14 @@ struct Model::Impl {
           }
           gemm1x1(kC3[li], rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
         } else {
-          if (rb.stride == 1 && rb.c1.frag && conv3x3_img_on) {
-            const Conv3x3Args a{x, Y1, nb, Fi, Ti, rb.c1.frag, rb.c1.bias, rb.c1.scale, rb.c1.shift};
+          if (rb.stride == 1 && img_ok(rb.c1, rb.planes)) {
+            const Conv3x3Args a{x, Y1, nb, Fi, Ti, rb.c1.frag, rb.c1.bias, rb.c1.scale, rb.c1.shift, nullptr, 1, conv3x3_img_on};
             run(kK3[li], 2.0 * nb * Fi * Ti * rb.c1.N * rb.c1.K, s, [&] { launch_conv3x3_img(a, rb.planes, s); });
           } else {
             gemm2d(kK3[li], rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
           }
-          if (rb.c2.frag && conv3x3_img_on && rb.out_planes == rb.planes) {
-            const Conv3x3Args a{Y1, o, nb, Fo, To, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, res};
+          if (img_ok(rb.c2, rb.planes) && rb.out_planes == rb.planes) {
+            const Conv3x3Args a{Y1, o, nb, Fo, To, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, res, 1, conv3x3_img_on};
             run(kK3[li], 2.0 * nb * Fo * To * rb.c2.N * rb.c2.K, s, [&] { launch_conv3x3_img(a, rb.planes, s); });
           } else {
             gemm2d(kK3[li], rb.c2, Y1, rb.planes, o, rb.out_planes, nb, Fo, To, 3, 1, 1, kActRelu, res,
@@ -824,14 +832,14 @@ struct Model::Impl {
           gemm2d("shortcut", rb.sc, x, Ci, SC, rb.planes, nb, Fi, Ti, 1, rb.stride, 0, kActNone, nullptr, 0, s);
           res = SC;
         }
-        if (rb.stride == 1 && rb.c1.frag && conv3x3_img_on) {
-          const Conv3x3Args a{x, Y1, nb, Fi, Ti, rb.c1.frag, rb.c1.bias, rb.c1.scale, rb.c1.shift};
+        if (rb.stride == 1 && img_ok(rb.c1, rb.planes)) {
+          const Conv3x3Args a{x, Y1, nb, Fi, Ti, rb.c1.frag, rb.c1.bias, rb.c1.scale, rb.c1.shift, nullptr, 1, conv3x3_img_on};
           run("res_conv3x3", 2.0 * nb * Fi * Ti * rb.c1.N * rb.c1.K, s, [&] { launch_conv3x3_img(a, rb.planes, s); });
         } else {
           gemm2d("res_conv3x3", rb.c1, x, Ci, Y1, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0, s);
         }
-        if (rb.c2.frag && conv3x3_img_on) {
-          const Conv3x3Args a{Y1, Z, nb, Fo, To, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, nullptr, 0};
+        if (img_ok(rb.c2, rb.planes)) {
+          const Conv3x3Args a{Y1, Z, nb, Fo, To, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, nullptr, 0, conv3x3_img_on};
           run("res_conv3x3", 2.0 * nb * Fo * To * rb.c2.N * rb.c2.K, s, [&] { launch_conv3x3_img(a, rb.planes, s); });
         } else {
           gemm2d("res_conv3x3", rb.c2, Y1, rb.planes, Z, rb.planes, nb, Fo, To, 3, 1, 1, kActNone, nullptr, 0, s);
@@ -909,6 +917,15 @@ struct Model::Impl {
       b.se2 = pack_lin(P(p + ".3.linear2.weight").data(), C, 128, 128, P(p + ".3.linear2.bias").data());
     }
     conv = pack_conv(P("conv.weight"), 1536, 3 * C, 1, P("conv.bias").data(), "");
+    {
+      std::vector<float> wg = P("conv.weight");  // [1536][3C]
+      for (int n = 0; n < 1536; ++n)
+        for (int c = 0; c < C; ++c) {
+          float* r = wg.data() + (size_t)n * 3 * C;
+          r[C + c] = (float)((double)r[C + c] + (double)r[2 * C + c]);
+        }
+      conv_g = pack_conv(wg, 1536, 3 * C, 1, P("conv.bias").data(), "");
+    }
     const auto& l1 = P("pool.linear1.weight");
     const int l1k = glob ? 4608 : 1536;
     {
@@ -1121,7 +1138,8 @@ struct Model::Impl {
         else launch_frame_stats(h3, C, B, T, C, gmean, C, 0, 0, s, seg);
         launch_small_linear({gmean, C, b.se1.wt, b.se1.bias, ghid, 128, B, C, 128, 1}, s);
         launch_small_linear({ghid, 128, b.se2.wt, b.se2.bias, gate, C, B, 128, C, 3}, s);
-        launch_residual_scale(xin, h3, gate, x[li + 2], B, T, C, s, seg, M);
+        // cat_gate: the last block stores only g4 * h3 (conv_cat adds out3 through its weights)
+        launch_residual_scale(cat_gate && li == 2 ? nullptr : xin, h3, gate, x[li + 2], B, T, C, s, seg, M);
       });
     }
     {
@@ -1135,8 +1153,9 @@ struct Model::Impl {
       g.cseg[1] = C;
       g.cseg[2] = 2 * C;
       g.cseg[3] = 3 * C;
-      fill(g, conv, M, T, 1, 0, xp, 1536, kActRelu, nullptr, true);
-      run("conv_cat", 2.0 * M * 1536 * 3 * C, s, [&] { launch(g, conv, s); });
+      const ConvW& cc = cat_gate ? conv_g : conv;
+      fill(g, cc, M, T, 1, 0, xp, 1536, kActRelu, nullptr, true);
+      run("conv_cat", 2.0 * M * 1536 * 3 * C, s, [&] { launch(g, cc, s); });
     }
     if (glob) {
       run("glob_ctx", 0, s, [&] {

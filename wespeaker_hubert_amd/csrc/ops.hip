@@ -223,6 +223,8 @@ void launch_frame_stats(const float* x, int ldx, int B, int T, int C, float* out
 namespace {
 constexpr int kRSRows = 64;  // rows per workgroup
 
+// HX = false: out = h * g (no residual operand)
+template <bool HX>
 __global__ __launch_bounds__(256) void residual_scale_kernel(const f32x4* __restrict__ x,
                                                              const f32x4* __restrict__ h,
                                                              const float* __restrict__ g,
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(256) void residual_scale_kernel(const f32x4* __rest
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const long i = (long)(r + u * rpp) * C4 + c4;
-        xv[u] = __builtin_nontemporal_load(x + i);
+        xv[u] = HX ? __builtin_nontemporal_load(x + i) : f32x4{0.f, 0.f, 0.f, 0.f};
         hv[u] = __builtin_nontemporal_load(h + i);
       }
 #pragma unroll
@@ -251,13 +253,13 @@ __global__ __launch_bounds__(256) void residual_scale_kernel(const f32x4* __rest
         gv[u] = *reinterpret_cast<const f32x4*>(g + ((long)b * C4 + c4) * 4);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) out[(long)(r + u * rpp) * C4 + c4] = xv[u] + hv[u] * gv[u];
+      for (int u = 0; u < 8; ++u) out[(long)(r + u * rpp) * C4 + c4] = HX ? xv[u] + hv[u] * gv[u] : hv[u] * gv[u];
     }
     for (; r < r1; r += rpp) {
       const int b = seg ? seg_of(seg, nseg, r) : r / T;
       const long i = (long)r * C4 + c4;
       const f32x4 gv = *reinterpret_cast<const f32x4*>(g + ((long)b * C4 + c4) * 4);
-      out[i] = x[i] + h[i] * gv;
+      out[i] = HX ? x[i] + h[i] * gv : h[i] * gv;
     }
   }
 }
@@ -270,9 +272,14 @@ void launch_residual_scale(const float* x, const float* h, const float* g, float
   WSP_CHECK(C4 % 256 == 0 || 256 % C4 == 0, "residual_scale: C/4 must divide or be a multiple of 256");
   const int rows = seg ? M : B * T;
   if (rows == 0) return;
-  hipLaunchKernelGGL(residual_scale_kernel, dim3(ceil_div(rows, kRSRows)), dim3(256), 0, s,
-                     reinterpret_cast<const f32x4*>(x), reinterpret_cast<const f32x4*>(h), g,
-                     reinterpret_cast<f32x4*>(out), rows, T, C4, seg, B);
+  const dim3 grid(ceil_div(rows, kRSRows));
+  const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+  const f32x4* h4 = reinterpret_cast<const f32x4*>(h);
+  f32x4* o4 = reinterpret_cast<f32x4*>(out);
+  if (x)
+    hipLaunchKernelGGL(residual_scale_kernel<true>, grid, dim3(256), 0, s, x4, h4, g, o4, rows, T, C4, seg, B);
+  else
+    hipLaunchKernelGGL(residual_scale_kernel<false>, grid, dim3(256), 0, s, x4, h4, g, o4, rows, T, C4, seg, B);
   WSP_HIP(hipGetLastError());
 }
 
