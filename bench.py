@@ -259,8 +259,10 @@ def plumbing_main(args):
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    check = rccl_check(torch.device("cpu"), world, rank) if world > 1 else None
     if rank == 0:
         print(json.dumps({"metric": "embeddings/sec on 5s 16kHz utts (plumbing rehearsal, no GPU work)",
+                          "rccl_allreduce_check": check,
                           "value": round(world * B * args.steps / el, 2), "unit": "emb/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(el / args.steps * 1e3, 3), "scaling": "weak",
@@ -268,6 +270,26 @@ def plumbing_main(args):
                                      "parallelism": f"dp{world}"}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def rccl_check(dev, world: int, rank: int) -> dict:
+    """Runs wespeaker_hubert_amd.dist.allreduce_sums on device buffers (rank r adds
+    r + 1 to a [G, D] sum and its counts) and compares with the closed form."""
+    import torch.distributed as tdist
+    from wespeaker_hubert_amd.dist import allreduce_sums
+    G, D = 1000, 192
+    acc = torch.full((G, D), float(rank + 1), dtype=torch.float64, device=dev)
+    cnt = torch.full((G,), float(rank + 1), dtype=torch.float64, device=dev)
+    t = time.perf_counter()
+    allreduce_sums(acc, cnt)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t) * 1e3
+    want = world * (world + 1) / 2
+    ok = torch.tensor([float(bool((acc == want).all()) and bool((cnt == want).all()))], device=dev)
+    tdist.all_reduce(ok, op=tdist.ReduceOp.MIN)
+    return {"backend": tdist.get_backend(), "world": world, "elements": G * D + G,
+            "ok": bool(ok.item() == 1.0), "ms_rank0": round(ms, 3)}
 
 
 def cpu_threads() -> int:
@@ -626,6 +648,14 @@ def main():
         "kernels": kernels,
         "cpu_baseline": None,
     }
+    if dist is not None:
+        # untimed: the AS-Norm cohort-statistics all-reduce (dist.allreduce_sums, one fused
+        # f64 buffer over RCCL/xGMI, score_norm.py's cohort means) on this run's ranks,
+        # checked against its closed form -- the one collective of the extraction path
+        try:
+            res["rccl_allreduce_check"] = rccl_check(dev, world, rank)
+        except Exception as e:  # reported, never fatal to the measurement above
+            res["rccl_allreduce_check"] = {"ok": False, "error": repr(e)[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = (cpu_baseline_hubert(sd_fe, sd, N, args.cpu_seconds) if hubert else
                                cpu_baseline(args.arch, sd, N, args.cpu_seconds))

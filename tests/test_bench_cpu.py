@@ -25,6 +25,9 @@ def test_bench_gpus2_launches_two_ranks():
     assert res["config"]["parallelism"] == "dp2"
     assert res["config"]["global_batch"] == 512
     assert res["steps"] == 3
+    # the cohort-statistics all-reduce (dist.allreduce_sums) ran on both ranks
+    chk = res["rccl_allreduce_check"]
+    assert chk["ok"] and chk["world"] == 2 and chk["backend"] == "gloo"
     # value = all ranks' utterances / max-over-ranks time (rank 1 sleeps longer)
     assert abs(res["value"] - 512 * 3 / (res["ms_per_step"] * 3e-3)) / res["value"] < 0.02
 

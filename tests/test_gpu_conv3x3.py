@@ -62,3 +62,23 @@ def test_conv3x3_img_batch_rows_equal_batch_of_one(img):
     for i in (0, 3, 5):
         one = img.embed(x[i:i + 1]).cpu().numpy()[0]
         assert np.array_equal(full[i], one)
+
+
+@pytest.mark.parametrize("arch,B,T", [("ResNet293", 2, 64), ("ResNet50", 3, 37), ("ResNet34", 2, 77)])
+def test_residual_prefetch_bit_identical(arch, B, T):
+    """Option res_prefetch (conv_gemm_x3 ROLE 2: the 1x1 residual convs load their
+    residual ahead of the last two k-tiles) changes only when the residual is read:
+    same products, same order, same epilogue -> identical embeddings."""
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    outs, sd = [], None
+    x = torch.from_numpy(synth_feats(12, B, T, 80)).to(DEV)
+    for on in (1, 0):
+        m = HipSpeakerModel(arch, feat_dim=80, embed_dim=256)
+        m.set_option("res_prefetch", on)
+        if sd is None:
+            sd = synth_state_dict(33, m.state_dict_layout(), residual_tame=True)
+        m.load_state_dict(sd)
+        m.to(DEV)
+        outs.append(m.embed(x).cpu().numpy())
+    assert np.all(np.isfinite(outs[0]))
+    assert np.array_equal(outs[0], outs[1])

@@ -187,6 +187,34 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   store_tile(ra0, rb0, 0);
   __syncthreads();
 
+  if constexpr (ROLE == 2) {
+    // residual convs (short K, the epilogue's residual read is a large part of a
+    // block): the last two k-tiles have no successors to load, so the residual
+    // loads go out in their place and land while those k-tiles multiply
+    for (int kt = 0; kt < nk - 2; kt += 2) {
+      load_tile(ra0, rb0, (kt + 2) * BK, true);
+      mma_step(0, 0);
+      store_tile(ra1, rb1, 1);
+      mma_step(0, 1);
+      __syncthreads();
+      load_tile(ra1, rb1, (kt + 3) * BK, true);
+      mma_step(1, 0);
+      store_tile(ra0, rb0, 0);
+      mma_step(1, 1);
+      __syncthreads();
+    }
+    float rv[TM][TN][16];
+    load_residual_tiles<TM, TN>(p, rv, m0, n0, wm, wn, lane);
+    mma_step(0, 0);
+    store_tile(ra1, rb1, 1);
+    mma_step(0, 1);
+    __syncthreads();
+    mma_step(1, 0);
+    mma_step(1, 1);
+    gemm_epilogue_res_pre<TM, TN>(p, acc, m0, n0, wm, wn, lane, rv);
+    return;
+  }
+
   // nk is even (Kp % 64 == 0, checked on the host).  Loads and stores are
   // unconditional (past-the-end tiles load zeros into a buffer nobody reads),
   // so the waitcnt pass sees one straight-line stream: the wait before
@@ -236,6 +264,12 @@ void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo,
     launch_x3_k<WM, WN, TM, TN, kACat, false, 0, false, SWZ, NSET>(p, whi, wlo, s);
   } else if (p.role == 1) {
     launch_x3_k<WM, WN, TM, TN, kACat, true, 1, false, SWZ, NSET>(p, whi, wlo, s);
+  } else if constexpr (NSET == 2 && TM * TN <= 4) {
+    // residual convs: the residual is loaded ahead of the last two k-tiles (ROLE 2)
+    if (p.res && p.role == 2)
+      launch_x3_k<WM, WN, TM, TN, kACat, true, 2, false, SWZ, NSET>(p, whi, wlo, s);
+    else
+      launch_x3_k<WM, WN, TM, TN, kACat, true, 0, false, SWZ, NSET>(p, whi, wlo, s);
   } else {
     launch_x3_k<WM, WN, TM, TN, kACat, true, 0, false, SWZ, NSET>(p, whi, wlo, s);
   }

@@ -201,9 +201,37 @@ struct ALoader2D {
 // s_memtime stamps) — and a row's byte offset is the tile's base plus a
 // compile-time row step times 4*ldo (no per-element multiply).  Rows >= M get
 // out-of-range buffer offsets: loads return 0, stores are dropped.
-template <int TM, int TN, int ACT, bool RB, bool CS = false, bool RES = false>
+// Residual rows of a wave's tiles in the accumulator layout (row (r&3) + 8(r>>2) + 4h
+// of tile i, column lane&31 of tile j): one b32 load per register.
+template <int TM, int TN>
+__device__ __forceinline__ void load_residual_tiles(const ConvGemmArgs& p, float (&rv)[TM][TN][16], int m0, int n0,
+                                                    int wm, int wn, int lane) {
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+  const __amdgpu_buffer_rsrc_t rres = make_rsrc(p.res);
+  const int ldr4 = p.ldres * 4;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row0 = m0 + (wm * TM + i) * 32 + 4 * h;
+      const int lim = p.M - row0;
+      const int rbase = row0 * ldr4 + (n0 + (wn * TN + j) * 32 + r32) * 4;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2);
+        rv[i][j][r] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rres, rr < lim ? rbase + rr * ldr4 : kOOB, 0, 0));
+      }
+    }
+}
+
+// PRE: the residual was loaded by the caller (rext, load_residual_tiles) ahead of
+// the last k-steps, so its latency overlaps them.
+template <int TM, int TN, int ACT, bool RB, bool CS = false, bool RES = false, bool PRE = false>
 __device__ __forceinline__ void gemm_epilogue_store(const ConvGemmArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0,
-                                                    int wm, int wn, int lane, double (*cs)[2] = nullptr) {
+                                                    int wm, int wn, int lane, double (*cs)[2] = nullptr,
+                                                    const float (*rext)[TN][16] = nullptr) {
   const int r32 = lane & 31;
   const int h = lane >> 5;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
@@ -215,7 +243,7 @@ __device__ __forceinline__ void gemm_epilogue_store(const ConvGemmArgs& p, f32x1
   const int ldr4 = p.ldres * 4;
   // narrow wave tiles (<= 4 tiles) can afford every residual load up front: one
   // round trip per wave instead of one per tile (HBM-bound ResNet conv3: -4 %)
-  constexpr bool RPRE = RES && TM * TN <= 4;
+  constexpr bool RPRE = RES && !PRE && TM * TN <= 4;
   float rpre[RPRE ? TM : 1][RPRE ? TN : 1][16];
   if constexpr (RPRE) {
 #pragma unroll
@@ -253,10 +281,13 @@ __device__ __forceinline__ void gemm_epilogue_store(const ConvGemmArgs& p, f32x1
         if (t0 + 32 <= p.M) mode = t0 + 32 <= next ? 0 : (t0 >= next ? 1 : 2);
       }
       float rv[16];
-      if constexpr (RPRE) {
+      if constexpr (PRE) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rv[r] = rext[i][j][r];
+      } else if constexpr (RPRE) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) rv[r] = rpre[i][j][r];
-      } else if constexpr (RES) {
+      } else if constexpr (RES && !PRE) {
         const int rbase = row0 * ldr4 + col * 4;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -371,6 +402,18 @@ __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&ac
       case kActGelu: gemm_epilogue_store<TM, TN, kActGelu, false>(p, acc, m0, n0, wm, wn, lane); break;
       default: gemm_epilogue_store<TM, TN, kActNone, false>(p, acc, m0, n0, wm, wn, lane); break;
     }
+  }
+}
+
+// Residual epilogue with the residual already in registers (see gemm_epilogue_store).
+template <int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue_res_pre(const ConvGemmArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0,
+                                                      int wm, int wn, int lane, const float (&rv)[TM][TN][16]) {
+  switch (p.act) {
+    case kActRelu: gemm_epilogue_store<TM, TN, kActRelu, false, false, true, true>(p, acc, m0, n0, wm, wn, lane, nullptr, rv); break;
+    case kActTanh: gemm_epilogue_store<TM, TN, kActTanh, false, false, true, true>(p, acc, m0, n0, wm, wn, lane, nullptr, rv); break;
+    case kActGelu: gemm_epilogue_store<TM, TN, kActGelu, false, false, true, true>(p, acc, m0, n0, wm, wn, lane, nullptr, rv); break;
+    default: gemm_epilogue_store<TM, TN, kActNone, false, false, true, true>(p, acc, m0, n0, wm, wn, lane, nullptr, rv); break;
   }
 }
 

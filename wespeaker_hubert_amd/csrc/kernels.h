@@ -40,7 +40,8 @@ struct ConvGemmArgs {
   int ldo;
   int act;
   int amode;
-  int role;  // 1 = SE-Res2Block 1x1 CxC conv (own kernel symbol for profiling)
+  int role;  // 1 = SE-Res2Block 1x1 CxC conv (own kernel symbol for profiling); 2 = residual
+             // conv whose residual is loaded ahead of the last two k-tiles (narrow bf16x3 tiles)
   // 2-D (NHWC, ResNet) mode: input [B][Fi][Ti][cin], output rows m = (b*Fo + fo)*To + to,
   // taps = kh*kw with tap j = kf*kw + kt, input (fo*stride + kf - pad, to*stride + kt - pad).
   int conv2d;

@@ -145,6 +145,7 @@ struct Model::Impl {
   // ResNet stride-1 3x3 convs on conv3x3_img.hip (option "conv3x3_img"): 0 = off (implicit GEMM),
   // 1 = 32 / 64 channels, 2 = also 128 channels (4 x 32 tile), 3 = also 128 (2 x 32 tile)
   int conv3x3_img_on = 2;
+  int res_prefetch = 1;  // ResNet 1x1 residual convs: residual loaded ahead of the last k-tiles (option "res_prefetch")
   bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
   int res2_variant = 0;  // res2_chain.hip kernel variant (option "res2_variant")
   ConvW conv, pool1, pool2;
@@ -598,6 +599,7 @@ struct Model::Impl {
     fill(g, cw, M, M, 1, 0, out, cw.N, act, nullptr, true);
     g.res = res;
     g.ldres = cw.N;
+    g.role = res && res_prefetch ? 2 : 0;
     run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_base(), s); });
   }
 
