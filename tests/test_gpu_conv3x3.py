@@ -82,3 +82,26 @@ def test_residual_prefetch_bit_identical(arch, B, T):
         outs.append(m.embed(x).cpu().numpy())
     assert np.all(np.isfinite(outs[0]))
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("arch,B,T", [("ResNet293", 2, 64), ("ResNet50", 3, 37), ("ResNet101", 1, 150)])
+def test_conv1x1_rows_bit_identical(arch, B, T):
+    """Option conv1x1_rows (the bottleneck conv1, 1x1 K -> K/4, from whole rows staged in
+    LDS, conv1x1_rows.hip) adds the same bf16x3 products in the same k order with the
+    same epilogue as conv_gemm_x3: identical embeddings, and the oracle bar holds."""
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    outs, sd = [], None
+    x = torch.from_numpy(synth_feats(13, B, T, 80)).to(DEV)
+    for on in (1, 0):
+        m = HipSpeakerModel(arch, feat_dim=80, embed_dim=256)
+        m.set_option("conv1x1_rows", on)
+        if sd is None:
+            sd = synth_state_dict(34, m.state_dict_layout(), residual_tame=True)
+        m.load_state_dict(sd)
+        m.to(DEV)
+        outs.append(m.embed(x).cpu().numpy())
+    assert np.all(np.isfinite(outs[0]))
+    assert np.array_equal(outs[0], outs[1])
+    with torch.no_grad():
+        _, ref = models_ref.forward(arch, x[:1].cpu(), {k: torch.from_numpy(v) for k, v in sd.items()})
+    assert np.abs(outs[0][:1] - ref.numpy()).max() < 1e-4

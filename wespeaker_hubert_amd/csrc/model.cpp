@@ -225,6 +225,9 @@ void Model::set_option(const std::string& key, int value) {
     for (const auto& p : impl->params) WSP_CHECK(!p.set, "option 'in_planes' must be set before the weights");
     impl->m_ch = value;
     impl->build_simam_params();
+  } else if (key == "conv1x1_rows") {
+    WSP_CHECK(value == 0 || value == 1, "conv1x1_rows must be 0 or 1");
+    impl->conv1x1_rows_on = value;
   } else if (key == "res_prefetch") {
     WSP_CHECK(value == 0 || value == 1, "res_prefetch must be 0 or 1");
     impl->res_prefetch = value;
@@ -265,6 +268,7 @@ int Model::get_option(const std::string& key) const {
   if (key == "res2_fused") return m.res2_fused;
   if (key == "cat_gate") return m.cat_gate;
   if (key == "res_prefetch") return m.res_prefetch;
+  if (key == "conv1x1_rows") return m.conv1x1_rows_on;
   if (key == "attn_lds") return m.attn_lds;
   if (key == "astp_fused") return m.astp_fused_on;
   if (key == "res2_variant") return m.res2_variant;

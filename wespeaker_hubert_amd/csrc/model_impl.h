@@ -18,6 +18,7 @@
 #include "res2_chain.h"
 #include "gemm_dma.h"
 #include "astp_fused.h"
+#include "conv1x1_rows.h"
 #include "conv3x3_img.h"
 
 namespace wsp {
@@ -55,7 +56,7 @@ struct ConvW {
   float* scale = nullptr;
   float* shift = nullptr;
   int N = 0, cin = 0, taps = 1, K = 0, Kp = 0;
-  void* frag = nullptr;  // 3x3, N = cin = 32 / 64: MFMA B-fragment order for conv3x3_img.hip
+  void* frag = nullptr;  // MFMA B-fragment order: 3x3 N = cin (conv3x3_img.hip), 1x1 (conv1x1_rows.hip)
 };
 
 struct LinW {  // small_linear weights, k-major
@@ -145,6 +146,7 @@ struct Model::Impl {
   // ResNet stride-1 3x3 convs on conv3x3_img.hip (option "conv3x3_img"): 0 = off (implicit GEMM),
   // 1 = 32 / 64 channels, 2 = also 128 channels (4 x 32 tile), 3 = also 128 (2 x 32 tile)
   int conv3x3_img_on = 2;
+  int conv1x1_rows_on = 0;  // ResNet conv1 (1x1 K -> K/4) on conv1x1_rows.hip (option "conv1x1_rows")
   int res_prefetch = 1;  // ResNet 1x1 residual convs: residual loaded ahead of the last k-tiles (option "res_prefetch")
   bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
   int res2_variant = 0;  // res2_chain.hip kernel variant (option "res2_variant")
@@ -450,6 +452,7 @@ struct Model::Impl {
     std::vector<float> b(N);
     for (int n = 0; n < N; ++n) b[n] = (float)sh[n];
     ConvW cw = pack_conv(w, N, cin, taps, b.data(), "");
+    if (taps == 1 && conv1x1_rows_supported(cin, N)) cw.frag = pack_frag(w, N, cin);  // k = c
     if (taps == 9 && N == cin && conv3x3_img_supported(cin)) {
       // the same k = tap * cin + c order as the implicit GEMM's packed image
       std::vector<float> wk((size_t)N * 9 * cin);
@@ -600,6 +603,12 @@ struct Model::Impl {
     g.res = res;
     g.ldres = cw.N;
     g.role = res && res_prefetch ? 2 : 0;
+    if (!res && act == kActRelu && cw.frag && cw.taps == 1 && conv1x1_rows_on) {
+      // whole rows staged in LDS (conv1x1_rows.hip): bit-identical to the GEMM below
+      const Conv1x1Args a{a0, out, M, cw.frag, cw.bias, cw.scale, cw.shift, 1};
+      run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv1x1_rows(a, cw.cin, cw.N, s); });
+      return;
+    }
     run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_base(), s); });
   }
 
