@@ -13,3 +13,7 @@ for v in 1 0; do
   timeout -k 10 200 python bench.py --arch ResNet293 --steps 10 --warmup 2 --no-cpu-baseline --no-f32 \
     --sustain-seconds 1 --opt conv1x1_rows=$v --opt streams=1 >> gpurun_out/c1r_c3_s1.jsonl 2> gpurun_out/c1r_s1_$v.err || exit 1
 done
+for v in 1 0; do
+  timeout -k 10 240 python bench.py --arch HuBERT_ECAPA_GLOB_c512 --steps 6 --warmup 2 --no-cpu-baseline --no-f32 \
+    --sustain-seconds 2 --opt cat_gate=$v >> gpurun_out/c4_cg.jsonl 2> gpurun_out/c4_cg_$v.err || exit 1
+done
