@@ -151,6 +151,11 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *                  patch (bit-identical to the implicit GEMM): 1 = 32 / 64 channels, 2 = also
  *                  128 channels, 4 x 32 positions x 4 column tiles per wave (default), 3 = also
  *                  128 channels, 8 waves x 2 column tiles; 0 = implicit GEMM throughout
+ *   "res_prefetch" ResNet: 1 = the 1x1 residual convs (bottleneck conv3) load their residual
+ *                  ahead of the last two k-tiles (default), 0 = in the epilogue (bit-identical)
+ *   "conv1x1_rows" ResNet: 1 = bottleneck conv1 (1x1, K -> K/4, K = 128 / 256 / 512) from whole
+ *                  rows staged in LDS (conv1x1_rows.hip; bit-identical, measured slower), 0 =
+ *                  the k-tiled GEMM (default)
  *   "cat_gate"     ECAPA-TDNN: 1 = conv_cat on [out2, out3, out4 - out3] with weights
  *                  [W_a, W_b + W_c, W_c], so the last SE block stores only its gated branch
  *                  (default; equal to 0 up to rounding, ~1e-6), 0 = conv_cat on [out2, out3, out4]
