@@ -59,7 +59,7 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
     WSP_CHECK(it != kRes.end(), "unsupported arch " + arch);
     WSP_CHECK(feat_dim >= 8, "ResNet feat_dim must be >= 8");
     m.ecapa = false;
-    m.x3_variant = 3;  // HBM-bound 1x1 convs: two 128 x 128 blocks per CU (+4 % over variant 4)
+    m.x3_variant = 4;  // 256 x 128 swizzled: with the residual prefetch (ROLE 2) +1.3 % C3 over variant 3 (r2c)
     m.streams = 2;     // two utterance ranges in flight: ResNet293 C3 +8.6 %
     m.bottleneck = it->second.first;
     for (int i = 0; i < 4; ++i) m.nblocks[i] = it->second.second[i];
