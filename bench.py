@@ -28,8 +28,8 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from wespeaker_hubert_amd.arch import (RESNET_ARCHS, ecapa_gflop_per_utt, hubert_gflop_per_utt, simam_gflop_per_utt,  # noqa: E402
-                                       make_spec)
+from wespeaker_hubert_amd.arch import (RESNET_ARCHS, ecapa_gflop_per_utt, hubert_gflop_per_utt,  # noqa: E402
+                                       make_spec, resnet_gflop_per_utt, simam_gflop_per_utt)
 from wespeaker_hubert_amd.frontend import compute_fbank  # noqa: E402
 from wespeaker_hubert_amd.s3prl_frontend import S3prlFrontend  # noqa: E402
 from wespeaker_hubert_amd.speaker_model import HipSpeakerModel  # noqa: E402
@@ -209,6 +209,12 @@ def parse():
     ap.add_argument("--no-f32", action="store_true", help="skip the exact-f32 (precision 0) side measurement")
     ap.add_argument("--sustain-seconds", type=float, default=2.0,
                     help="extra untimed-for-value window reported as value_sustained (>= this many seconds)")
+    ap.add_argument("--configs", default="C3,C4",
+                    help="sub-configurations timed after the C2 headline (C3 = ResNet293 B=128, C4 = HuBERT-base + "
+                         "ECAPA_TDNN_GLOB_c512 B=256), comma-separated, or 'none'")
+    ap.add_argument("--sub-steps", type=int, default=10)
+    ap.add_argument("--sub-warmup", type=int, default=2)
+    ap.add_argument("--sub-cpu-seconds", type=float, default=10.0)
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU/gloo rehearsal of the rank launch, barriers and JSON (no GPU work; tests only)")
     return ap.parse_args()
@@ -311,10 +317,10 @@ def cpu_threads() -> int:
     return max(1, n)
 
 
-def cpu_baseline(arch: str, sd, num_samples: int, budget_s: float):
+def cpu_baseline(arch: str, sd, num_samples: int, budget_s: float, batch: int = 8):
     """Oracle ('port') pipeline timed on the host cores: numpy float64 fbank +
-    CMN, then the fp32 PyTorch-CPU restatement of the reference ECAPA forward.
-    Bounded sample: batches of 8 utterances until >= budget_s of work."""
+    CMN, then the fp32 PyTorch-CPU restatement of the reference forward (ECAPA /
+    ResNet).  Bounded sample: batches of `batch` utterances until >= budget_s of work."""
     from oracle import fbank_ref, models_ref
     threads = cpu_threads()
     torch.set_num_threads(threads)
@@ -326,16 +332,16 @@ def cpu_baseline(arch: str, sd, num_samples: int, budget_s: float):
         with torch.no_grad():
             models_ref.forward(arch, torch.from_numpy(feats), sdt)
 
-    run(2, 1000)  # warm-up
+    run(min(2, batch), 1000)  # warm-up
     done, t0 = 0, time.perf_counter()
     while True:
-        run(8, 1001 + done)
-        done += 8
+        run(batch, 1001 + done)
+        done += batch
         el = time.perf_counter() - t0
         if el >= budget_s or done >= 256:
             break
     return {"value": done / el, "unit": "emb/s", "cores": threads, "kind": "port", "os_cpu_count": os.cpu_count(),
-            "sample": f"{done} synthetic {num_samples / 16000:.0f}s utts, batches of 8, "
+            "sample": f"{done} synthetic {num_samples / 16000:.0f}s utts, batches of {batch}, "
                       f"numpy-f64 fbank + torch-CPU fp32 {arch} (oracle restatement), {el:.1f}s"}
 
 
@@ -367,35 +373,21 @@ def cpu_baseline_hubert(sd_fe, sd, num_samples: int, budget_s: float):
                       f"HuBERT-base + s3prl glue + CMN + ECAPA_TDNN_GLOB_c512 (oracle restatement), {el:.1f}s"}
 
 
-def main():
-    args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args.gpus))
-    if args.plumbing:
-        return plumbing_main(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+# Sub-configurations reported beside the headline (BASELINE.json configs[2] and [3]):
+# name -> (arch, per-GPU batch).  C4's per-GPU batch is 256 like C2 (SURVEY §8(d) quotes
+# 64: with 64 utterances fc2 / out_proj fill 189 of the 256 CUs, with 256 they fill 2.9
+# rounds, +12.5 % -- DESIGN.md §5)
+SUB_CONFIGS = {"C3": ("ResNet293", 128), "C4": (HUBERT_ARCH, 256)}
 
-    hubert = args.arch == HUBERT_ARCH
-    simam = args.arch.startswith("SimAM")
-    resnet_like = args.arch.startswith("ResNet") or simam
-    global PROFILE_TAG
-    PROFILE_TAG = {"ECAPA_TDNN_c1024": "c2", "ResNet293": "c3", HUBERT_ARCH: "c4"}.get(args.arch, "none")
-    # C4 per GPU: 256 utterances like C2 (fc2 / out_proj have 3 column tiles of 256:
-    # 64 utterances fill 189 of the 256 CUs; 256 fill 2.9 rounds; +12.5 % over 64)
-    B = args.batch or (128 if resnet_like else 256)
+
+def build_workload(args, arch: str, B: int, rank: int, dev):
+    """Model(s), synthetic HBM-resident inputs and the step closure of one workload."""
+    hubert = arch == HUBERT_ARCH
+    simam = arch.startswith("SimAM")
+    resnet_like = arch.startswith("ResNet") or simam
     N = int(round(args.seconds * 16000))
     emb_dim = 256 if resnet_like else 192
-    head_arch = "ECAPA_TDNN_GLOB_c512" if hubert else args.arch
+    head_arch = "ECAPA_TDNN_GLOB_c512" if hubert else arch
     feat_dim = 768 if hubert else 80
     margs = dict(acoustic_dim=feat_dim, embed_dim=emb_dim) if simam else dict(feat_dim=feat_dim, embed_dim=emb_dim)
     spec = make_spec(head_arch, **margs)
@@ -417,7 +409,6 @@ def main():
             k, _, v = kv.partition("=")
             mm.set_option(k, int(v))
         mm.to(dev)
-
     # inputs resident in HBM before the timed region (per-rank shard)
     wav = torch.from_numpy(synth_audio(7 + rank, B, N, int16_scale=not hubert)).to(dev)
     T = (N + 319) // 320 if hubert else 1 + (N - 400) // 160
@@ -431,36 +422,203 @@ def main():
             compute_fbank(wav, scale=1.0, cmn=True, out=feats)
         model.embed(feats, out=emb)
 
+    return dict(arch=arch, head_arch=head_arch, hubert=hubert, simam=simam, resnet_like=resnet_like, B=B, N=N, T=T,
+                spec=spec, model=model, fe=fe, sd=sd, sd_fe=sd_fe, step=step, wav=wav, feats=feats, emb=emb)
+
+
+def kernel_table(w, steps: int) -> dict:
+    """Per kernel class: launches, average launch time (HIP events on the launch
+    stream, wsp_model_profile), time per step and the class's algorithmic rate."""
+    kernels = {}
+    queries = [(w["model"], t) for t in HEAD_TAGS] + ([(w["fe"], t) for t in HUBERT_TAGS] if w["fe"] else [])
+    for mm, tag in queries:
+        n, ms, fl = mm.profile_query(tag)
+        if n:
+            avg = ms / n
+            kernels[tag] = {"launches_per_step": n // steps, "avg_ms": round(avg, 4),
+                            "ms_per_step": round(ms / steps, 4),
+                            "tflops": round(fl / (avg * 1e-3) / 1e12, 2) if fl else None,
+                            "flops_per_launch": fl or None}
+    return kernels
+
+
+def dominant_class(kernels: dict, streams: int) -> dict:
+    """The kernel class with the most launch time per step (a top-level class, not a
+    per-stage sub-class); with concurrent streams the summed launch times of both
+    utterance ranges are compared (they overlap in wall time)."""
+    top = {k: v for k, v in kernels.items() if "." not in k}
+    if not top:
+        return None
+    name = max(top, key=lambda k: top[k]["ms_per_step"])
+    d = {"class": name, **top[name]}
+    if d.get("tflops"):
+        d["frac_of_bf16_peak"] = round(d["tflops"] / BF16_MFMA_PEAK_TFLOPS, 4)
+        d["frac_of_issue_peak"] = round(3 * d["tflops"] / BF16_MFMA_PEAK_TFLOPS, 4)
+    if streams > 1:
+        d["note"] = (f"launch times summed over {streams} concurrent utterance-range streams; "
+                     "per-launch rates are measured while the other range's kernels share the GPU")
+    return d
+
+
+def roofline_ecapa(args, w, k, streams):
+    """Per-kernel MFMA roofline of the SE-Res2Block 1x1 CxC conv (the headline's dominant kernel)."""
+    C = 1024 if "c1024" in w["arch"] else 512
+    M = w["B"] * w["T"] // streams   # rows per launch (one utterance range)
+    flops = 2.0 * M * C * C          # algorithmic: 2*M*N*K, M = B*T frames
+    ach = flops / (k["avg_ms"] * 1e-3) / 1e12
+    x3 = args.precision == 1
+    peak = BF16_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+    sym, bm, bn, nt = dominant_symbol(args.precision, args.x3_variant, C, C, 1)
+    grid = ((M + bm - 1) // bm) * (C // bn) * nt
+    traffic, src = profiled_traffic(sym, grid)
+    algo_bytes = 4.0 * M * C * 2 + (2 if x3 else 4) * C * C * (2 if x3 else 1)
+    return {"kernel": sym, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+            "traffic": traffic, "traffic_source": src, "algorithmic_bytes": algo_bytes,
+            "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"],
+            "mfma_dtype": "bf16 (3-term split, fp32 accumulate)" if x3 else "f32",
+            "mfma_work_factor": 3 if x3 else 1,
+            "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4), **pmc_fields(sym, grid),
+            "concurrent_streams": streams}
+
+
+def roofline_resnet_model(args, w, kernels, el, steps, streams):
+    """C3: whole-model HBM roofline -- every conv's algorithmic fp32 bytes of a step
+    (resnet_model_bytes_per_utt x B) over the measured step time, independent of how
+    launches overlap; the 1x1-conv class figure (summed launch time) beside it."""
+    arch, B, T, model = w["arch"], w["B"], w["T"], w["model"]
+    mb = resnet_model_bytes_per_utt(arch, 80, T) * B
+    ms_step = el / steps * 1e3
+    ach = mb / (ms_step * 1e-3) / 1e9
+    roof = {"kernel": "whole ResNet forward (fbank + stem + every conv + TSTP), algorithmic bytes / step time",
+            "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_step": mb, "ms_per_step": round(ms_step, 3),
+            "traffic": None,
+            "bytes_note": "fp32 activations: each conv's input read once, output written once, the bottleneck "
+                          "conv3's residual read once, the pooling read; weights excluded (L2-resident)"}
+    kr = kernels.get("res_conv1x1")
+    if not kr:
+        return roof
+    bc = B // -(-B // 64) if B > 64 else B  # the model's 2-GiB chunking at T = 498
+    geo = resnet_1x1_launch_geometry(arch, 80, T, bc)
+    traffic_step, srcs = 0.0, set()
+    for tag, bpu in resnet_1x1_bytes_by_stage(arch, 80, T).items():
+        n, ms, _ = model.profile_query(tag)
+        if not n:
+            continue
+        kernels[tag] = {"launches_per_step": n // steps, "avg_ms": round(ms / n, 4),
+                        "ms_per_step": round(ms / steps, 4),
+                        "gbps": round(bpu * B / (ms / steps * 1e-3) / 1e9, 1)}
+        if traffic_step is not None and tag in geo:
+            chunks = (n // steps) // sum(c for _, _, c in geo[tag])
+            for sym, grid, cnt in geo[tag]:
+                tb, src = profiled_traffic(sym, grid)
+                if tb is None:
+                    traffic_step = None
+                    break
+                traffic_step += tb * cnt * chunks
+                srcs.add(src.split(":")[0])
+    for li in range(1, 5):
+        n, ms, fl = model.profile_query(f"res_conv3x3.L{li}")
+        if n:
+            kernels[f"res_conv3x3.L{li}"] = {"launches_per_step": n // steps, "avg_ms": round(ms / n, 4),
+                                             "ms_per_step": round(ms / steps, 4),
+                                             "tflops": round(fl / (ms / n * 1e-3) / 1e12, 2)}
+    byts = resnet_1x1_bytes_per_utt(arch, 80, T) * B
+    a1 = byts / (kr["ms_per_step"] * 1e-3) / 1e9
+    roof["class_1x1"] = {"kernel": "conv_gemm_x3 ResNet 1x1 convs (res_conv1x1, all launches of a step)",
+                         "achieved": round(a1, 1), "frac": round(a1 / HBM_PEAK_GBPS, 4),
+                         "algorithmic_bytes": byts, "launches_per_step": kr["launches_per_step"],
+                         "ms_per_step": kr["ms_per_step"], "traffic": traffic_step or None,
+                         "traffic_source": ",".join(sorted(srcs)) or None,
+                         "traffic_note": "PMC HBM bytes of all 1x1 launches of a step (FETCH_SIZE x2 + WRITE_SIZE)"}
+    if streams > 1:
+        roof["class_1x1"]["note"] = ("launch durations measured beside the other utterance range's kernels "
+                                     "(option streams); --opt streams=1 gives the standalone rate")
+    return roof
+
+
+def roofline_model_mfma(args, w, gf_utt, el, steps):
+    """C4: model-level MFMA roofline -- the whole chain's algorithmic FLOP per step
+    (HuBERT-base + ECAPA head, 2 x MACs) over the measured step time, against the dense
+    bf16 peak; the issued fraction (3 bf16 MFMAs per fp32 product) beside it."""
+    B = w["B"]
+    flops = gf_utt * 1e9 * B
+    ms_step = el / steps * 1e3
+    ach = flops / (ms_step * 1e-3) / 1e12
+    x3 = args.precision == 1
+    peak = BF16_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+    return {"kernel": "whole HuBERT-base + CMN + ECAPA_TDNN_GLOB_c512 chain, algorithmic FLOP / step time",
+            "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "algorithmic_flops_per_step": flops, "ms_per_step": round(ms_step, 3),
+            "mfma_dtype": "bf16 (3-term split, fp32 accumulate)" if x3 else "f32",
+            "mfma_work_factor": 3 if x3 else 1, "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4),
+            "traffic": None}
+
+
+def roofline_simam(args, k3):
+    ach = k3["tflops"] or 0.0
+    x3 = args.precision == 1
+    return {"kernel": "conv_gemm_x3 SimAM-ResNet 3x3 convs (res_conv3x3, all launches of a step)",
+            "bound": "mfma", "achieved": ach, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": None, "traffic_source": None,
+            "launches_per_step": k3["launches_per_step"], "ms_per_step": k3["ms_per_step"],
+            "mfma_dtype": "bf16 (3-term split, fp32 accumulate)", "mfma_work_factor": 3 if x3 else 1,
+            "frac_of_issue_peak": round(ach * 3 / BF16_MFMA_PEAK_TFLOPS, 4)}
+
+
+def gflop_per_utt(w) -> float:
+    arch, spec, T, N = w["arch"], w["spec"], w["T"], w["N"]
+    if w["hubert"]:
+        return hubert_gflop_per_utt(N) + ecapa_gflop_per_utt(spec, T)
+    if arch.startswith("ECAPA"):
+        return ecapa_gflop_per_utt(spec, T)
+    if w["simam"]:
+        return simam_gflop_per_utt(spec, T)
+    return resnet_gflop_per_utt(spec, T)
+
+
+def run_workload(args, arch: str, B: int, steps: int, warmup: int, world: int, rank: int, dev, dist,
+                 headline: bool, cpu_seconds: float) -> dict:
+    """One workload: W untimed warm-up steps, then K steps timed between barrier +
+    synchronize, max over ranks; per-kernel-class HIP events inside the timed region."""
+    w = build_workload(args, arch, B, rank, dev)
+    model, fe, step = w["model"], w["fe"], w["step"]
+
     def barrier():
         torch.cuda.synchronize(dev)
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
+    def max_over_ranks(e):
+        if dist is not None:
+            t = torch.tensor([e], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e = float(t.item())
+        return e
+
+    for _ in range(warmup):
         step()
     barrier()
     # Per-kernel-class HIP events are recorded on the launch stream around
     # every launch inside the timed region (wsp_model_profile); they feed the
     # roofline figure below.
     if not args.no_profile:
-        model.profile(True)
-        if fe is not None:
-            fe.profile(True)
+        for mm in (model, fe):
+            if mm is not None:
+                mm.profile(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     barrier()
     el = time.perf_counter() - t0
     if not args.no_profile:
-        model.profile(False)
-        if fe is not None:
-            fe.profile(False)
-    if dist is not None:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    value = world * B * args.steps / el
+        for mm in (model, fe):
+            if mm is not None:
+                mm.profile(False)
+    el = max_over_ranks(el)
+    value = world * B * steps / el
 
     def timed(n):
         barrier()
@@ -468,30 +626,24 @@ def main():
         for _ in range(n):
             step()
         barrier()
-        e = time.perf_counter() - t
-        if dist is not None:
-            tt = torch.tensor([e], device=dev, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            e = float(tt.item())
-        return e
+        return max_over_ranks(time.perf_counter() - t)
 
-    # sustained window (>= --sustain-seconds of back-to-back steps, profiling
-    # off): the same step count on every rank, derived from the max-over-ranks time
-    sustained = None
-    if args.sustain_seconds > 0:
-        n_s = max(args.steps, int(np.ceil(args.sustain_seconds / (el / args.steps))))
+    sustained = exact = None
+    if headline and args.sustain_seconds > 0:
+        # >= --sustain-seconds of back-to-back steps, profiling off: the same step
+        # count on every rank, derived from the max-over-ranks time
+        n_s = max(steps, int(np.ceil(args.sustain_seconds / (el / steps))))
         e_s = timed(n_s)
         sustained = {"value": round(world * B * n_s / e_s, 2), "steps": n_s, "seconds": round(e_s, 3),
                      "ms_per_step": round(e_s / n_s * 1e3, 3)}
-    # exact-f32 MFMA (precision 0) beside the bf16x3 headline
-    exact = None
-    if args.precision == 1 and not args.no_f32:
+    if headline and args.precision == 1 and not args.no_f32:
+        # exact-f32 MFMA (precision 0) beside the bf16x3 headline
         for mm in (model, fe):
             if mm is not None:
                 mm.set_option("precision", 0)
                 mm.to(dev)
         step()
-        n_f = max(2, args.steps // 4)
+        n_f = max(2, steps // 4)
         e_f = timed(n_f)
         exact = {"value": round(world * B * n_f / e_f, 2), "steps": n_f,
                  "ms_per_step": round(e_f / n_f * 1e3, 3), "dtype": "f32 (v_mfma_f32_32x32x2_f32)"}
@@ -500,154 +652,119 @@ def main():
     # with more than one, per-launch durations are measured while another range's
     # kernels share the GPU, so per-kernel roofline fractions read low
     streams = max(m.get_option("streams") for m in (model, fe) if m is not None)
+    gf = gflop_per_utt(w)
     kernels, roof = {}, None
     if not args.no_profile:
-        queries = [(model, t) for t in HEAD_TAGS] + ([(fe, t) for t in HUBERT_TAGS] if fe is not None else [])
-        for mm, tag in queries:
-            n, ms, fl = mm.profile_query(tag)
-            if n:
-                avg = ms / n
-                kernels[tag] = {"launches_per_step": n // args.steps, "avg_ms": round(avg, 4),
-                                "ms_per_step": round(ms / args.steps, 4),
-                                "tflops": round(fl / (avg * 1e-3) / 1e12, 2) if fl else None,
-                                "flops_per_launch": fl or None}
-        k = kernels.get("h_fc1") if hubert else kernels.get("conv1x1_CxC")
-        kr = kernels.get("res_conv1x1") if args.arch.startswith("ResNet") else None
-        k3 = kernels.get("res_conv3x3") if simam else None
-        traffic_step, traffic_srcs = 0.0, set()
-        if kr:
-            # per-stage HBM rate of the 1x1 convs (sub-classes of res_conv1x1), and the
-            # class's PMC traffic per step: profiled bytes per launch of each sub-class's
-            # (symbol, grid) x its launches per step
-            bc = B // -(-B // 64) if B > 64 else B  # the model's 2-GiB chunking at T = 498
-            geo = resnet_1x1_launch_geometry(args.arch, 80, T, bc)
-            for tag, bpu in resnet_1x1_bytes_by_stage(args.arch, 80, T).items():
-                n, ms, _ = model.profile_query(tag)
-                if n:
-                    kernels[tag] = {"launches_per_step": n // args.steps, "avg_ms": round(ms / n, 4),
-                                    "ms_per_step": round(ms / args.steps, 4),
-                                    "gbps": round(bpu * B / (ms / args.steps * 1e-3) / 1e9, 1)}
-                    if traffic_step is not None and tag in geo:
-                        chunks = (n // args.steps) // sum(c for _, _, c in geo[tag])
-                        for sym, grid, cnt in geo[tag]:
-                            tb, src = profiled_traffic(sym, grid)
-                            if tb is None:
-                                traffic_step = None
-                                break
-                            traffic_step += tb * cnt * chunks
-                            traffic_srcs.add(src.split(":")[0])
-            for li in range(1, 5):
-                n, ms, fl = model.profile_query(f"res_conv3x3.L{li}")
-                if n:
-                    kernels[f"res_conv3x3.L{li}"] = {"launches_per_step": n // args.steps, "avg_ms": round(ms / n, 4),
-                                                     "ms_per_step": round(ms / args.steps, 4),
-                                                     "tflops": round(fl / (ms / n * 1e-3) / 1e12, 2)}
-        if k3:
-            # MFMA roofline of the SimAM-ResNet 3x3 convs as a class (all launches of a step)
-            ach = k3["tflops"] or 0.0
-            x3 = args.precision == 1
-            roof = {"kernel": "conv_gemm_x3 SimAM-ResNet 3x3 convs (res_conv3x3, all launches of a step)",
-                    "bound": "mfma", "achieved": ach, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": None, "traffic_source": None,
-                    "launches_per_step": k3["launches_per_step"], "ms_per_step": k3["ms_per_step"],
-                    "mfma_dtype": "bf16 (3-term split, fp32 accumulate)", "mfma_work_factor": 3 if x3 else 1,
-                    "frac_of_issue_peak": round(ach * 3 / BF16_MFMA_PEAK_TFLOPS, 4)}
-        elif kr:
-            # HBM roofline of the ResNet 1x1 convs as a class (all launches of a step)
-            byts = resnet_1x1_bytes_per_utt(args.arch, 80, T) * B
-            ach = byts / (kr["ms_per_step"] * 1e-3) / 1e9
-            roof = {"kernel": "conv_gemm_x3 ResNet 1x1 convs (res_conv1x1, all launches of a step)",
-                    "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic_step or None,
-                    "traffic_source": ",".join(sorted(traffic_srcs)) or None,
-                    "traffic_note": "PMC HBM bytes of all 1x1 launches of a step (FETCH_SIZE x2 + WRITE_SIZE)",
-                    "algorithmic_bytes": byts, "launches_per_step": kr["launches_per_step"],
-                    "ms_per_step": kr["ms_per_step"],
-                    "concurrent_streams": streams}
-            # whole-model byte roofline: every conv's algorithmic bytes of a step over the
-            # measured step time (fbank included), independent of how launches overlap
-            mb = resnet_model_bytes_per_utt(args.arch, 80, T) * B
-            if mb and el > 0:
-                mg = mb / (el / args.steps) / 1e9
-                roof["model"] = {"algorithmic_bytes_per_step": mb, "achieved": round(mg, 1),
-                                 "frac": round(mg / HBM_PEAK_GBPS, 4)}
-            if streams > 1:
-                roof["note"] = ("launch durations measured beside the other utterance range's kernels "
-                                "(option streams); --opt streams=1 gives the standalone rate")
-        elif k and hubert:
-            Th = (N - 400) // 320 + 1  # HuBERT conv frames (249 for 5 s)
-            M, Nn, K = B * Th // streams, 3072, 768  # rows per launch (one utterance range)
-            flops = 2.0 * M * Nn * K
-            ach = flops / (k["avg_ms"] * 1e-3) / 1e12
-            x3 = args.precision == 1
-            peak = BF16_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
-            sym, bm, bn, nt = dominant_symbol(args.precision, args.x3_variant, Nn, K, 0)
-            grid = ((M + bm - 1) // bm) * (Nn // bn) * nt
-            traffic, src = profiled_traffic(sym, grid)
-            roof = {"kernel": sym + " (HuBERT FFN fc1 + GELU)", "bound": "mfma", "achieved": round(ach, 2),
-                    "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
-                    "traffic_source": src, "algorithmic_bytes": 4.0 * M * (K + Nn) + (4 if x3 else 4) * Nn * K,
-                    "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"],
-                    "mfma_dtype": "bf16 (3-term split, fp32 accumulate)" if x3 else "f32",
-                    "mfma_work_factor": 3 if x3 else 1,
-                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4), **pmc_fields(sym, grid),
-                    "concurrent_streams": streams}
-        elif k:
-            C = 1024 if "c1024" in args.arch else 512
-            M = B * T // streams             # rows per launch (one utterance range)
-            flops = 2.0 * M * C * C          # algorithmic: 2*M*N*K, M = B*T frames
-            ach = flops / (k["avg_ms"] * 1e-3) / 1e12
-            x3 = args.precision == 1
-            peak = BF16_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
-            sym, bm, bn, nt = dominant_symbol(args.precision, args.x3_variant, C, C, 1)
-            grid = ((M + bm - 1) // bm) * (C // bn) * nt
-            traffic, src = profiled_traffic(sym, grid)
-            algo_bytes = 4.0 * M * C * 2 + (2 if x3 else 4) * C * C * (2 if x3 else 1)
-            roof = {"kernel": sym, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                    "traffic": traffic, "traffic_source": src, "algorithmic_bytes": algo_bytes,
-                    "flops_per_launch": flops, "avg_launch_ms": k["avg_ms"],
-                    "mfma_dtype": "bf16 (3-term split, fp32 accumulate)" if x3 else "f32",
-                    "mfma_work_factor": 3 if x3 else 1,
-                    "frac_of_issue_peak": round(ach * (3 if x3 else 1) / peak, 4), **pmc_fields(sym, grid),
-                    "concurrent_streams": streams}
-        if roof is not None and streams > 1 and "note" not in roof:
+        kernels = kernel_table(w, steps)
+        if w["hubert"]:
+            roof = roofline_model_mfma(args, w, gf, el, steps)
+        elif arch.startswith("ResNet"):
+            roof = roofline_resnet_model(args, w, kernels, el, steps, streams)
+        elif w["simam"] and kernels.get("res_conv3x3"):
+            roof = roofline_simam(args, kernels["res_conv3x3"])
+        elif kernels.get("conv1x1_CxC"):
+            roof = roofline_ecapa(args, w, kernels["conv1x1_CxC"], streams)
+        if roof is not None and streams > 1 and "note" not in roof and not w["resnet_like"] and not w["hubert"]:
             roof["note"] = ("launch durations measured beside the other utterance range's kernels "
                             "(option streams); --opt streams=1 gives the standalone rate")
+    res = {
+        "value": round(value, 2),
+        "ms_per_step": round(el / steps * 1e3, 3),
+        "steps": steps,
+        "warmup": warmup,
+        "workload": (f"HuBERT-base (s3prl featurizer) + CMN + ECAPA_TDNN_GLOB_c512 extract, "
+                     f"{args.seconds:g}s 16kHz utts" if w["hubert"] else
+                     f"{arch} fbank80 extract, {args.seconds:g}s 16kHz utts"),
+        "arch": arch, "batch_per_gpu": B, "global_batch": B * world,
+        "samples_per_utt": w["N"], "frames": w["T"], "streams": streams,
+        "model_tflops": round(value * gf / 1e3, 2),
+        "gflop_per_utt": round(gf, 3),
+        "roofline": roof,
+        "dominant_class": dominant_class(kernels, streams) if kernels else None,
+        "kernels": kernels,
+        "value_sustained": sustained,
+        "value_exact_f32": exact,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = (cpu_baseline_hubert(w["sd_fe"], w["sd"], w["N"], cpu_seconds) if w["hubert"] else
+                               cpu_baseline(arch, w["sd"], w["N"], cpu_seconds,
+                                            batch=2 if w["resnet_like"] else 8))
+    # free the workload's device buffers before the next one
+    for key in ("model", "fe"):
+        if w[key] is not None:
+            w[key]._release()
+    del w
+    torch.cuda.empty_cache()
+    return res
 
-    gf = hubert_gflop_per_utt(N) + ecapa_gflop_per_utt(spec, T) if hubert else ecapa_gflop_per_utt(spec, T) \
-        if args.arch.startswith("ECAPA") else simam_gflop_per_utt(spec, T) if simam else sum(
-        v["ms_per_step"] * (v.get("tflops") or 0) for k, v in kernels.items() if "." not in k) / B \
-        if kernels else 0.0
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if args.plumbing:
+        return plumbing_main(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    arch = args.arch
+    hubert = arch == HUBERT_ARCH
+    resnet_like = arch.startswith("ResNet") or arch.startswith("SimAM")
+    global PROFILE_TAG
+    PROFILE_TAG = {"ECAPA_TDNN_c1024": "c2", "ResNet293": "c3", HUBERT_ARCH: "c4"}.get(arch, "none")
+    B = args.batch or (128 if resnet_like else 256)
+    r = run_workload(args, arch, B, args.steps, args.warmup, world, rank, dev, dist, headline=True,
+                     cpu_seconds=args.cpu_seconds)
     res = {
         "metric": "embeddings/sec on 5s 16kHz utts",
-        "value": round(value, 2),
+        "value": r["value"],
         "unit": "emb/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "ms_per_step": r["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32 (bf16x3 split MFMA, fp32 accumulate)" if args.precision == 1 else "f32",
-        "value_sustained": sustained,
-        "value_exact_f32": exact,
+        "value_sustained": r["value_sustained"],
+        "value_exact_f32": r["value_exact_f32"],
         "data": ("synthetic (clip(N(0,0.1)) [-1,1] audio, seeded random-init weights)" if hubert else
                  "synthetic (clip(N(0,0.1)) x32768 PCM16-valued audio, seeded random-init weights)"),
-        "config": {"workload": (f"HuBERT-base (s3prl featurizer) + CMN + ECAPA_TDNN_GLOB_c512 extract, "
-                                f"{args.seconds:g}s 16kHz utts" if hubert else
-                                f"{args.arch} fbank80 extract, {args.seconds:g}s 16kHz utts"),
-                   "arch": args.arch, "batch_per_gpu": B, "global_batch": B * world,
-                   "samples_per_utt": N, "frames": T, "parallelism": f"dp{world}",
-                   "streams": streams},
-        "model_tflops": round(value * gf / 1e3, 2),
-        "gflop_per_utt": round(gf, 3),
-        "roofline": roof,
+        "config": {"workload": r["workload"], "arch": arch, "batch_per_gpu": B, "global_batch": B * world,
+                   "samples_per_utt": r["samples_per_utt"], "frames": r["frames"], "parallelism": f"dp{world}",
+                   "streams": r["streams"]},
+        "model_tflops": r["model_tflops"],
+        "gflop_per_utt": r["gflop_per_utt"],
+        "roofline": r["roofline"],
+        "dominant_class": r["dominant_class"],
         "options": args.opt or None,
-        "kernels": kernels,
-        "cpu_baseline": None,
+        "kernels": r["kernels"],
+        "cpu_baseline": r["cpu_baseline"],
     }
+    # the other single-GPU-per-rank configurations of BASELINE.json (C3 ResNet293,
+    # C4 HuBERT + ECAPA), each timed the same way (own warm-up, barrier-bracketed
+    # steps, max over ranks), with its own roofline and CPU baseline
+    subs = [s for s in args.configs.split(",") if s and s != "none"] if arch == "ECAPA_TDNN_c1024" else []
+    if subs:
+        res["configs"] = {}
+        for name in subs:
+            if name not in SUB_CONFIGS:
+                raise SystemExit(f"bench.py: unknown --configs entry {name} (known: {sorted(SUB_CONFIGS)})")
+            sarch, sb = SUB_CONFIGS[name]
+            PROFILE_TAG = name.lower()
+            res["configs"][name] = run_workload(args, sarch, sb, args.sub_steps, args.sub_warmup, world, rank, dev,
+                                                dist, headline=False, cpu_seconds=args.sub_cpu_seconds)
     if dist is not None:
         # untimed: the AS-Norm cohort-statistics all-reduce (dist.allreduce_sums, one fused
         # f64 buffer over RCCL/xGMI, score_norm.py's cohort means) on this run's ranks,
@@ -656,9 +773,6 @@ def main():
             res["rccl_allreduce_check"] = rccl_check(dev, world, rank)
         except Exception as e:  # reported, never fatal to the measurement above
             res["rccl_allreduce_check"] = {"ok": False, "error": repr(e)[:300]}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = (cpu_baseline_hubert(sd_fe, sd, N, args.cpu_seconds) if hubert else
-                               cpu_baseline(args.arch, sd, N, args.cpu_seconds))
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:

@@ -204,6 +204,30 @@ def simam_gflop_per_utt(spec: ModelSpec, T: int) -> float:
     return 2.0 * macs / 1e9
 
 
+def resnet_gflop_per_utt(spec: ModelSpec, T: int) -> float:
+    """Algorithmic FLOPs (2 x MACs) of one ResNet forward over T frames (resnet.py:35-204):
+    stem, every block's convs (+ projection shortcuts), the pooled-statistics embedding."""
+    kind, nblocks = RESNET_ARCHS[spec.arch]
+    m, F, t = spec.m_channels, spec.feat_dim, T
+    exp = 1 if kind == "basic" else 4
+    macs = F * t * m * 9  # stem 3x3, 1 -> m
+    cin = m
+    for li, n in enumerate(nblocks):
+        p = m * (2 ** li)
+        for bi in range(n):
+            s = 2 if (li > 0 and bi == 0) else 1
+            Fo, To = (F - 1) // s + 1, (t - 1) // s + 1
+            if kind == "basic":
+                macs += Fo * To * p * (cin * 9 + p * 9)
+            else:
+                macs += F * t * cin * p + Fo * To * (p * p * 9 + p * 4 * p)
+            if s != 1 or cin != exp * p:
+                macs += Fo * To * cin * exp * p
+            F, t, cin = Fo, To, exp * p
+    macs += 2 * cin * F * spec.embed_dim + (spec.embed_dim ** 2 if spec.two_emb_layer else 0)
+    return 2.0 * macs / 1e9
+
+
 def ecapa_gflop_per_utt(spec: ModelSpec, T: int) -> float:
     """Algorithmic FLOPs (2 x MACs) of one ECAPA forward over T frames."""
     C, glob = ECAPA_ARCHS[spec.arch]
