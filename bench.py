@@ -58,7 +58,7 @@ def dominant_symbol(precision: int, variant, N: int, K: int, role: int):
     return sym, bm, bn, nt
 HUBERT_ARCH = "HuBERT_ECAPA_GLOB_c512"  # C4: HuBERT-base front end + ECAPA_TDNN_GLOB_c512(feat_dim 768)
 HEAD_TAGS = ("layer1", "conv1x1_CxC", "res2_k3", "se", "conv_cat", "glob_ctx", "pool_linear1", "pool_linear2",
-             "astp", "head", "stem", "shortcut", "res_conv1x1", "res_conv3x3", "tstp_head",
+             "astp", "head", "stem", "shortcut", "res_conv1x1", "res_conv3x3", "res_tail", "tstp_head",
              "simam", "asp_rows", "asp_linear1", "asp_linear2", "asp_pool_head")
 HUBERT_TAGS = ("h_conv0", "h_cnn", "h_ln", "h_proj", "h_pos_conv", "h_qkv", "h_attn", "h_out_proj", "h_fc1",
                "h_fc2", "h_cmn")
@@ -501,16 +501,24 @@ def roofline_resnet_model(args, w, kernels, el, steps, streams):
         return roof
     bc = B // -(-B // 64) if B > 64 else B  # the model's 2-GiB chunking at T = 498
     geo = resnet_1x1_launch_geometry(arch, 80, T, bc)
-    traffic_step, srcs = 0.0, set()
+    traffic_step, srcs, byts = 0.0, set(), 0.0
+    chunks = -(-B // bc)
     for tag, bpu in resnet_1x1_bytes_by_stage(arch, 80, T).items():
         n, ms, _ = model.profile_query(tag)
         if not n:
             continue
+        # with res_tail the stride-1 blocks' conv3 runs inside bottleneck_tail: only the
+        # stride-2 first blocks' conv3 launches remain (same output shape as the others)
+        expected = chunks * sum(c for _, _, c in geo[tag])
+        bts = bpu * B * (n // steps) / expected
+        byts += bts
         kernels[tag] = {"launches_per_step": n // steps, "avg_ms": round(ms / n, 4),
                         "ms_per_step": round(ms / steps, 4),
-                        "gbps": round(bpu * B / (ms / steps * 1e-3) / 1e9, 1)}
-        if traffic_step is not None and tag in geo:
-            chunks = (n // steps) // sum(c for _, _, c in geo[tag])
+                        "gbps": round(bts / (ms / steps * 1e-3) / 1e9, 1)}
+        if traffic_step is not None:
+            if n // steps != expected:
+                traffic_step = None  # PMC summaries are per launch geometry of the unfused schedule
+                continue
             for sym, grid, cnt in geo[tag]:
                 tb, src = profiled_traffic(sym, grid)
                 if tb is None:
@@ -518,13 +526,13 @@ def roofline_resnet_model(args, w, kernels, el, steps, streams):
                     break
                 traffic_step += tb * cnt * chunks
                 srcs.add(src.split(":")[0])
-    for li in range(1, 5):
-        n, ms, fl = model.profile_query(f"res_conv3x3.L{li}")
-        if n:
-            kernels[f"res_conv3x3.L{li}"] = {"launches_per_step": n // steps, "avg_ms": round(ms / n, 4),
-                                             "ms_per_step": round(ms / steps, 4),
-                                             "tflops": round(fl / (ms / n * 1e-3) / 1e12, 2)}
-    byts = resnet_1x1_bytes_per_utt(arch, 80, T) * B
+    for cls in ("res_conv3x3", "res_tail"):
+        for li in range(1, 5):
+            n, ms, fl = model.profile_query(f"{cls}.L{li}")
+            if n:
+                kernels[f"{cls}.L{li}"] = {"launches_per_step": n // steps, "avg_ms": round(ms / n, 4),
+                                           "ms_per_step": round(ms / steps, 4),
+                                           "tflops": round(fl / (ms / n * 1e-3) / 1e12, 2)}
     a1 = byts / (kr["ms_per_step"] * 1e-3) / 1e9
     roof["class_1x1"] = {"kernel": "conv_gemm_x3 ResNet 1x1 convs (res_conv1x1, all launches of a step)",
                          "achieved": round(a1, 1), "frac": round(a1 / HBM_PEAK_GBPS, 4),

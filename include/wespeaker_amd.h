@@ -135,27 +135,23 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *                  slice, so query the workspace size after setting it); results are
  *                  bit-identical to 1.  Default 2 for ResNet / SimAM-ResNet / HuBERT,
  *                  1 for ECAPA-TDNN; segmented ECAPA batches always run as one range
- *   "x3_variant"   bf16x3 conv-GEMM tile: 0 = 128x128, 1 = 256x128, 3 = 128x128 with
- *                  swizzled LDS rows (ResNet default), 4 = 256x128 swizzled,
- *                  5 = 256x256 where N % 256 == 0 (default), 6 = 256x128 one staging
- *                  set, 2 / 9 = LDS-DMA staged variants where supported
+ *   "x3_variant"   bf16x3 conv-GEMM tile family (all with swizzled LDS rows): 3 = 128x128,
+ *                  4 = 256x128 (ResNet default), 5 = 256x256 where N % 256 == 0, else 256x128
+ *                  (ECAPA-TDNN, SimAM-ResNet and HuBERT default)
  *   "res2_fused"   1 = one res2_chain launch per SE_Res2Block (default), 0 = 7 GEMMs
  *   "res2_variant" res2_chain tile: 0 = 128 rows, 2 waves on N (default), 1 = 256 rows,
  *                  2 = 128 rows, 4 waves on N (C = 128 only)
- *   "astp_fused"   ASTP linear2 + softmax statistics in one kernel: 1 = 128 channels per
- *                  block, 2 = 256 channels with att chunks shared through LDS-DMA, 3 = 2 with
- *                  W2 in registers and a deeper ring (default; all three bit-identical);
- *                  0 = linear2 GEMM + separate pooling kernel
- *   "attn_lds"     HuBERT: 1 = K / V staged once per 256-key block in LDS (default)
+ *   "astp_fused"   ECAPA-TDNN ASTP linear2 + softmax statistics in one kernel (astp_fused.hip,
+ *                  default 1); 0 = linear2 GEMM + separate pooling kernel
  *   "conv3x3_img"  ResNet / SimAM-ResNet stride-1 3x3 convs from an LDS image of the input
  *                  patch (bit-identical to the implicit GEMM): 1 = 32 / 64 channels, 2 = also
  *                  128 channels, 4 x 32 positions x 4 column tiles per wave (default), 3 = also
  *                  128 channels, 8 waves x 2 column tiles; 0 = implicit GEMM throughout
  *   "res_prefetch" ResNet: 1 = the 1x1 residual convs (bottleneck conv3) load their residual
  *                  ahead of the last two k-tiles (default), 0 = in the epilogue (bit-identical)
- *   "conv1x1_rows" ResNet: 1 = bottleneck conv1 (1x1, K -> K/4, K = 128 / 256 / 512) from whole
- *                  rows staged in LDS (conv1x1_rows.hip; bit-identical, measured slower), 0 =
- *                  the k-tiled GEMM (default)
+ *   "res_tail"     ResNet: 1 = the bottleneck conv2 (3x3) + conv3 (1x1) + residual + ReLU of
+ *                  stride-1 blocks with 32 / 64 / 128 planes in one launch, conv2's output kept in
+ *                  registers (default); 0 = conv2 and conv3 as separate launches through HBM
  *   "cat_gate"     ECAPA-TDNN: 1 = conv_cat on [out2, out3, out4 - out3] with weights
  *                  [W_a, W_b + W_c, W_c], so the last SE block stores only its gated branch
  *                  (default; equal to 0 up to rounding, ~1e-6), 0 = conv_cat on [out2, out3, out4]

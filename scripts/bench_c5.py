@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--trials", type=int, default=37611)
     ap.add_argument("--top-n", type=int, default=300)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=1, help="untimed passes of the whole pipeline first")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -73,51 +74,58 @@ def main():
 
     # this rank's shard of the eval audio, resident in HBM before the clock starts
     wavs = [torch.from_numpy(synth_audio(1000 + b0, min(a.batch, hi - b0), N)).to(dev) for b0 in range(lo, hi, a.batch)]
-    model.embed(compute_fbank(wavs[0][:2], scale=1.0, cmn=True))  # warm-up
     n_rows = 2 * a.cohort  # cohort utterance embeddings (synthetic), this rank's shard in HBM
     clo, chi = wdist.shard_bounds(n_rows, rank, world)
     g = np.arange(n_rows, dtype=np.int32) // 2
     xs = torch.from_numpy(np.random.default_rng(7).standard_normal((n_rows, D)).astype(np.float32)[clo:chi]).to(dev)
-    times = {}
-    sync()
-    t0 = time.perf_counter()
-    # ---- extract (per-rank shard, batches of a.batch)
-    mine = [model.embed(compute_fbank(w, scale=1.0, cmn=True)) for w in wavs]
-    mine = torch.cat(mine) if mine else torch.empty(0, D, device=dev)
-    if world > 1:
-        per = a.eval_utts // world + 1
-        pad = torch.zeros(per, D, device=dev)
-        pad[:mine.shape[0]] = mine
-        gathered = [torch.empty_like(pad) for _ in range(world)]
-        torch.distributed.all_gather(gathered, pad)
-        E = torch.cat([g[:wdist.shard_bounds(a.eval_utts, r, world)[1] - wdist.shard_bounds(a.eval_utts, r, world)[0]]
-                       for r, g in enumerate(gathered)])
-    else:
-        E = mine
-    sync()
-    times["extract"] = time.perf_counter() - t0
-    # ---- cohort means: 2 synthetic utterance embeddings per speaker, sharded sums + one all-reduce
-    t1 = time.perf_counter()
-    acc, cnt = group_sums(xs, g[clo:chi], a.cohort)
-    wdist.allreduce_sums(acc, cnt)
-    C = (acc / cnt.unsqueeze(1)).float()
-    sync()
-    times["cohort"] = time.perf_counter() - t1
-    # ---- scoring: mean vector, cosine trials, AS-Norm stats (top-n), normalised scores
-    t2 = time.perf_counter()
-    mean_vec = E.double().mean(0).float()
-    En = l2_normalize(E, mean_vec)
-    s = cosine_pairs(En, trials_a, trials_b)
-    mu, sd = asnorm_stats(E, C, a.top_n, mean_vec)
-    ns = 0.5 * ((s - mu[trials_a]) / sd[trials_a] + (s - mu[trials_b]) / sd[trials_b])
-    sync()
-    times["score"] = time.perf_counter() - t2
-    t3 = time.perf_counter()
-    fnr, fpr = compute_pmiss_pfa_rbst(ns, labels)
-    eer, thr = compute_eer(fnr, fpr, ns)
-    mindcf = compute_c_norm(fnr, fpr, 0.01)
-    times["metrics"] = time.perf_counter() - t3
-    total = time.perf_counter() - t0
+    def run_once():
+        times = {}
+        sync()
+        t0 = time.perf_counter()
+        # ---- extract (per-rank shard, batches of a.batch)
+        mine = [model.embed(compute_fbank(w, scale=1.0, cmn=True)) for w in wavs]
+        mine = torch.cat(mine) if mine else torch.empty(0, D, device=dev)
+        if world > 1:
+            per = a.eval_utts // world + 1
+            pad = torch.zeros(per, D, device=dev)
+            pad[:mine.shape[0]] = mine
+            gathered = [torch.empty_like(pad) for _ in range(world)]
+            torch.distributed.all_gather(gathered, pad)
+            E = torch.cat([g[:wdist.shard_bounds(a.eval_utts, r, world)[1] - wdist.shard_bounds(a.eval_utts, r, world)[0]]
+                           for r, g in enumerate(gathered)])
+        else:
+            E = mine
+        sync()
+        times["extract"] = time.perf_counter() - t0
+        # ---- cohort means: 2 synthetic utterance embeddings per speaker, sharded sums + one all-reduce
+        t1 = time.perf_counter()
+        acc, cnt = group_sums(xs, g[clo:chi], a.cohort)
+        wdist.allreduce_sums(acc, cnt)
+        C = (acc / cnt.unsqueeze(1)).float()
+        sync()
+        times["cohort"] = time.perf_counter() - t1
+        # ---- scoring: mean vector, cosine trials, AS-Norm stats (top-n), normalised scores
+        t2 = time.perf_counter()
+        mean_vec = E.double().mean(0).float()
+        En = l2_normalize(E, mean_vec)
+        s = cosine_pairs(En, trials_a, trials_b)
+        mu, sd = asnorm_stats(E, C, a.top_n, mean_vec)
+        ns = 0.5 * ((s - mu[trials_a]) / sd[trials_a] + (s - mu[trials_b]) / sd[trials_b])
+        sync()
+        times["score"] = time.perf_counter() - t2
+        t3 = time.perf_counter()
+        fnr, fpr = compute_pmiss_pfa_rbst(ns, labels)
+        eer, thr = compute_eer(fnr, fpr, ns)
+        mindcf = compute_c_norm(fnr, fpr, 0.01)
+        times["metrics"] = time.perf_counter() - t3
+        total = time.perf_counter() - t0
+        return times, total, eer, mindcf
+
+    # every stage once untimed (kernel code objects, the top-n workspace, RCCL's first
+    # all-reduce, host allocators), then the timed pass
+    for _ in range(a.warmup):
+        run_once()
+    times, total, eer, mindcf = run_once()
     if world > 1:
         t = torch.tensor([total] + [times[k] for k in ("extract", "cohort", "score", "metrics")], device=dev,
                          dtype=torch.float64)
@@ -132,6 +140,7 @@ def main():
                           "trials_per_s": round(a.trials / times["score"], 1),
                           "eval_emb_per_s": round(a.eval_utts / times["extract"], 1),
                           "eer": float(eer), "min_dcf": float(mindcf),
+                          "warmup_passes": a.warmup,
                           "config": {"arch": a.arch, "eval_utts": a.eval_utts, "seconds": a.seconds,
                                      "cohort": a.cohort, "trials": a.trials, "top_n": a.top_n},
                           "data": "synthetic audio / cohort embeddings / random trial labels"}), flush=True)

@@ -34,7 +34,9 @@ def test_compute_metrics_runs_from_a_recipe_symlink(tmp_path):
 
 
 def test_every_recipe_entry_point_has_a_launcher():
-    for m in ("extract", "score", "score_norm", "compute_metrics", "score_calibration"):
+    # every wespeaker/bin script the recipes' extraction / scoring stages call
+    # (tools/extract_embedding.sh, local/score.sh, score_norm.sh, score_calibration.sh)
+    for m in ("extract", "score", "score_norm", "compute_metrics", "compute_det", "score_calibration"):
         assert os.path.isfile(os.path.join(REPO, "compat", "wespeaker", "bin", m + ".py"))
         assert os.path.isfile(os.path.join(REPO, "wespeaker_hubert_amd", "bin", m + ".py"))
 
@@ -45,3 +47,18 @@ def test_import_wespeaker_exports_the_reference_names(tmp_path):
                           "callable(wespeaker.load_model_pt))"], cwd=d, capture_output=True, text=True,
                          check=True).stdout
     assert out.split() == ["wespeaker_hubert_amd", "True"]
+
+
+def test_compute_det_writes_the_det_plot(tmp_path):
+    """local/score.sh:54 `python wespeaker/bin/compute_det.py <scores>` -> <scores>.det.png."""
+    d = _recipe(tmp_path)
+    rng = np.random.default_rng(1)
+    with open(d / "trials.score", "w") as f:
+        for i in range(300):
+            tgt = i % 3 == 0
+            f.write(f"e{i} t{i} {rng.normal(0.5 if tgt else 0.0, 0.2):.5f} {'target' if tgt else 'nontarget'}\n")
+    out = subprocess.run([sys.executable, "wespeaker/bin/compute_det.py", "trials.score"], cwd=d, capture_output=True,
+                         text=True, check=True).stdout
+    png = d / "trials.score.det.png"
+    assert "DET curve saved in trials.score.det.png" in out
+    assert png.is_file() and png.read_bytes()[:8] == b"\x89PNG\r\n\x1a\n"

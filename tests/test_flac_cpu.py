@@ -99,6 +99,28 @@ def test_corruption_is_detected():
         decode_flac(bytes(data[:-10]))
 
 
+
+def test_id3_tags_around_the_stream_are_skipped():
+    """A leading ID3v2 tag (syncsafe size, with and without its footer flag) and a
+    trailing ID3v1 'TAG' block, which common decoders tolerate, decode to the
+    untagged stream's samples."""
+    x = _signal(1, 3000, 16, 11)
+    data = encode_flac(x, 16000, 16, [1000, 1000, 1000])
+    body = b"TIT2" + (5).to_bytes(4, "big") + b"\x00\x00" + b"\x00test"   # one text frame
+    body += bytes(300)                                                   # padding
+    sz = len(body)
+    syncsafe = bytes([(sz >> 21) & 0x7F, (sz >> 14) & 0x7F, (sz >> 7) & 0x7F, sz & 0x7F])
+    v1 = b"TAG" + bytes(125)
+    for flags, footer in ((0x00, b""), (0x10, b"3DI\x04\x00\x10" + syncsafe)):
+        tagged = b"ID3\x04\x00" + bytes([flags]) + syncsafe + body + footer + data + v1
+        y, rate, bits = decode_flac(tagged)
+        assert (rate, bits) == (16000, 16)
+        np.testing.assert_array_equal(y, x)
+    # padding after the last frame ends the stream once STREAMINFO's count is decoded
+    y, _, _ = decode_flac(data + bytes(64))
+    np.testing.assert_array_equal(y, x)
+
+
 def test_load_audio_flac_matches_torchaudio_conventions():
     x16 = _signal(1, 2000, 16, 11)
     d16 = encode_flac(x16, 16000, 16, [2000])

@@ -134,7 +134,26 @@ def test_cli_embedding_kaldi(model_dir, wav_scp, tmp_path):
     got = dict(load_scp_sequential(out + ".scp"))
     assert sorted(got) == sorted(pcms)
     for k, e in got.items():
-        assert _cos(e, _oracle_embed(sd, pcms[k])) >= 0.9999
+        ref = _oracle_embed(sd, pcms[k])
+        assert _cos(e, ref) >= 0.9999
+        assert np.abs(e - ref).max() < 1e-4
+
+
+def _oracle_chunks(pcms_in_list_order, chunk_len, seed=0):
+    """processor.py:291-323 get_random_chunk, driven like bin/extract.py's chunking
+    (one draw per utterance in data-list order from a Random(seed) stream; shorter
+    utterances repeat-padded without a draw)."""
+    import random
+    rng = random.Random(seed)
+    out = []
+    for x in pcms_in_list_order:
+        n = len(x)
+        if n >= chunk_len:
+            st = rng.randint(0, n - chunk_len)
+            out.append(x[st:st + chunk_len])
+        else:
+            out.append(np.tile(x, chunk_len // n + 1)[:chunk_len])
+    return out
 
 
 @pytest.mark.parametrize("batch_size", [1, 4])
@@ -149,8 +168,19 @@ def test_extract_driver_raw_list(model_dir, wav_scp, tmp_path, batch_size):
     assert sorted(got) == sorted(pcms)
     if batch_size == 1:
         for k, e in got.items():
-            assert _cos(e, _oracle_embed(sd, pcms[k])) >= 0.9999
-    else:  # random 2.0 s chunks: deterministic for a fixed chunk_seed
+            ref = _oracle_embed(sd, pcms[k])
+            assert _cos(e, ref) >= 0.9999
+            assert np.abs(e - ref).max() < 1e-4
+    else:
+        # random 2.0 s chunks (num_frms 200: 32 240 samples), one per utterance in list
+        # order: the same chunks as an oracle chunking of the same seed
+        keys = sorted(pcms)
+        chunks = _oracle_chunks([pcms[k] for k in keys], (199 * 10 + 25) * 16)
+        for k, c in zip(keys, chunks):
+            ref = _oracle_embed(sd, c)
+            assert _cos(got[k], ref) >= 0.9999
+            assert np.abs(got[k] - ref).max() < 1e-4, k
+        # deterministic for a fixed chunk_seed
         scp2 = extract(config=os.path.join(d, "config.yaml"), model_path=os.path.join(d, "avg_model.pt"),
                        data_type="raw", data_list=raw, embed_ark=str(tmp_path / "x2.ark"), batch_size=batch_size)
         got2 = dict(load_scp_sequential(scp2))
@@ -311,3 +341,57 @@ def test_vector_mean_sharded_allreduce_world2(tmp_path):
         np.testing.assert_allclose(res[r], single, atol=1e-6)
     got = dict(load_scp_sequential(str(tmp_path / "dist.scp")))
     assert sorted(got) == sorted(spk)
+
+
+def test_recipe_extract_embedding_sh_two_shards(model_dir, wav_scp, tmp_path):
+    """tools/extract_embedding.sh:40-62 unedited, through a recipe `wespeaker`
+    symlink to compat/wespeaker: `split -l` of the raw data list into nj = 2
+    contiguous shards, one `python -u wespeaker/bin/extract.py` per shard with the
+    script's exact flag set (batch size 1, 1 worker, reverb / noise lists,
+    aug-prob 0), both in flight at once, then `cat xvector_*.scp`; every row equals
+    the oracle chain at the north-star bar (per-dim 1e-4, cosine 0.9999)."""
+    import subprocess
+    import sys
+    d, sd = model_dir
+    _, raw, pcms = wav_scp
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rec = tmp_path / "recipe"
+    rec.mkdir()
+    os.symlink(os.path.join(repo, "compat", "wespeaker"), rec / "wespeaker")
+    embed_dir = rec / "exp" / "embeddings" / "vox1"
+    log_dir = embed_dir / "log"
+    log_dir.mkdir(parents=True)
+    nj = 2
+    script = f"""set -e
+data_num=$(wc -l {raw} | awk '{{print $1}}')
+subfile_num=$(($data_num / {nj} + 1))
+split -l ${{subfile_num}} -d -a 3 {raw} {log_dir}/split_
+for suffix in $(seq 0 $(({nj} - 1))); do
+  suffix=$(printf '%03d' $suffix)
+  {sys.executable} -u wespeaker/bin/extract.py \\
+    --config {d}/config.yaml \\
+    --model_path {d}/avg_model.pt \\
+    --data_type raw \\
+    --data_list {log_dir}/split_${{suffix}} \\
+    --embed_ark {embed_dir}/xvector_${{suffix}}.ark \\
+    --batch-size 1 \\
+    --num-workers 1 \\
+    --reverb_data data/rirs/lmdb \\
+    --noise_data data/musan/lmdb \\
+    --aug-prob 0.0 \\
+    >{log_dir}/split_${{suffix}}.log 2>&1 &
+done
+wait
+cat {embed_dir}/xvector_*.scp >{embed_dir}/xvector.scp
+"""
+    r = subprocess.run(["bash", "-c", script], cwd=rec, capture_output=True, text=True, timeout=600)
+    logs = "".join(open(log_dir / f).read() for f in sorted(os.listdir(log_dir)) if f.endswith(".log"))
+    assert r.returncode == 0, r.stderr + logs
+    assert sorted(os.listdir(log_dir)) == ["split_000", "split_000.log", "split_001", "split_001.log"]
+    got = list(load_scp_sequential(str(embed_dir / "xvector.scp")))
+    keys = [k for k, _ in got]
+    assert keys == sorted(pcms)  # shard 0 rows, then shard 1 rows: the list order
+    for k, e in got:
+        ref = _oracle_embed(sd, pcms[k])
+        assert _cos(e, ref) >= 0.9999
+        assert np.abs(e - ref).max() < 1e-4, k

@@ -26,6 +26,8 @@ def _pair(arch, seed, img=1):
     for on in (img, 0):
         m = HipSpeakerModel(arch, feat_dim=80, embed_dim=256)
         m.set_option("conv3x3_img", on)
+        if not arch.startswith("SimAM"):
+            m.set_option("res_tail", 0)  # the image kernel alone (the fused tail: test_res_tail_*)
         if sd is None:
             sd = synth_state_dict(seed, m.state_dict_layout(), residual_tame=True)
         m.load_state_dict(sd)
@@ -84,24 +86,45 @@ def test_residual_prefetch_bit_identical(arch, B, T):
     assert np.array_equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("arch,B,T", [("ResNet293", 2, 64), ("ResNet50", 3, 37), ("ResNet101", 1, 150)])
-def test_conv1x1_rows_bit_identical(arch, B, T):
-    """Option conv1x1_rows (the bottleneck conv1, 1x1 K -> K/4, from whole rows staged in
-    LDS, conv1x1_rows.hip) adds the same bf16x3 products in the same k order with the
-    same epilogue as conv_gemm_x3: identical embeddings, and the oracle bar holds."""
+
+def _tail_pair(arch, seed, feat_dim):
     from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
-    outs, sd = [], None
-    x = torch.from_numpy(synth_feats(13, B, T, 80)).to(DEV)
+    ms, sd = [], None
     for on in (1, 0):
-        m = HipSpeakerModel(arch, feat_dim=80, embed_dim=256)
-        m.set_option("conv1x1_rows", on)
+        m = HipSpeakerModel(arch, feat_dim=feat_dim, embed_dim=256)
+        m.set_option("res_tail", on)
         if sd is None:
-            sd = synth_state_dict(34, m.state_dict_layout(), residual_tame=True)
+            sd = synth_state_dict(seed, m.state_dict_layout(), residual_tame=True)
         m.load_state_dict(sd)
-        m.to(DEV)
-        outs.append(m.embed(x).cpu().numpy())
-    assert np.all(np.isfinite(outs[0]))
-    assert np.array_equal(outs[0], outs[1])
+        ms.append(m.to(DEV))
+    return ms[0], ms[1], sd
+
+
+# feat_dim 40: stage 3 runs at F = 10, a partial 4-row frequency tile; T = 37 / 100 / 150
+# leave partial 32- / 64-frame time tiles
+@pytest.mark.parametrize("arch,B,T,F", [("ResNet50", 3, 100, 80), ("ResNet50", 2, 37, 40),
+                                        ("ResNet101", 1, 150, 80), ("ResNet293", 2, 64, 80),
+                                        ("ResNet152", 2, 45, 40)])
+def test_res_tail_matches_unfused_and_oracle(arch, B, T, F):
+    """Option res_tail (conv3x3_img.hip bottleneck_tail: conv2 + conv3 + residual in one
+    launch, conv2's output kept in registers as conv3's A operand with a permuted k
+    order) against the two-launch path (conv3x3_img + conv_gemm_x3) and the oracle.
+    The same bf16x3 products are summed in a different k order inside conv3's MFMAs, so
+    the two agree to fp32 rounding, not bitwise."""
+    tail, plain, sd = _tail_pair(arch, 41, F)
+    x = torch.from_numpy(synth_feats(19, B, T, F)).to(DEV)
+    a = tail.embed(x).cpu().numpy()
+    b = plain.embed(x).cpu().numpy()
+    assert np.all(np.isfinite(a))
+    assert np.abs(a - b).max() <= 2e-5 * max(1.0, float(np.abs(b).max())), np.abs(a - b).max()
     with torch.no_grad():
-        _, ref = models_ref.forward(arch, x[:1].cpu(), {k: torch.from_numpy(v) for k, v in sd.items()})
-    assert np.abs(outs[0][:1] - ref.numpy()).max() < 1e-4
+        _, ref = models_ref.forward(arch, x.cpu(), {k: torch.from_numpy(v) for k, v in sd.items()})
+    assert np.abs(a - ref.numpy()).max() < 1e-4
+
+
+def test_res_tail_batch_rows_equal_batch_of_one():
+    tail, _, _ = _tail_pair("ResNet50", 42, 80)
+    x = torch.from_numpy(synth_feats(20, 5, 123, 80)).to(DEV)
+    full = tail.embed(x).cpu().numpy()
+    for i in (0, 2, 4):
+        assert np.array_equal(full[i], tail.embed(x[i:i + 1]).cpu().numpy()[0])

@@ -164,17 +164,13 @@ def test_ragged_batch_equals_batch_of_one(sd_np, sd_t, layer, multi):
 
 
 @pytest.mark.parametrize("W", [16000, 100000])
-def test_lds_attention_matches_streaming_kernel_and_oracle(sd_np, sd_t, W):
-    """attn.hip (K / V staged once per 256-key block in LDS) against the streaming
-    mha_kernel (option attn_lds=0) and the oracle; W = 100000 gives 312 frames:
-    two query blocks and two key blocks per (utterance, head)."""
+def test_lds_attention_matches_oracle(sd_np, sd_t, W):
+    """attn.hip (K / V staged once per 256-key block in LDS) against the oracle;
+    W = 100000 gives 312 frames: two query blocks and two key blocks per
+    (utterance, head)."""
     wav = _wav(17, 2, W)
     fe = _frontend(sd_np)
     got = fe.extract(torch.from_numpy(wav).to(DEV)).cpu()
-    fe0 = _frontend(sd_np)
-    fe0.set_option("attn_lds", 0)
-    old = fe0.extract(torch.from_numpy(wav).to(DEV)).cpu()
-    assert float((got - old).abs().max()) < 2e-5
     with torch.no_grad():
         ref = hubert_ref.s3prl_frontend(torch.from_numpy(wav), sd_t)
     assert float((got - ref).abs().max()) < FEAT_ATOL

@@ -2,7 +2,7 @@
 // not part of the product).  Plain GEMM shapes (taps = 1) or 1-D convs:
 //   gemm_bench M N K [taps [reps]] ...   (K = cin * taps)
 // For every kernel variant: average launch time over `reps` launches with HIP
-// events, algorithmic TFLOP/s (2*M*N*K), and max |diff| against variant 1.
+// events, algorithmic TFLOP/s (2*M*N*K), and max |diff| against variant 4.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -96,14 +96,13 @@ int main(int argc, char** argv) {
     struct V {
       const char* name;
       int kind;
-    } vars[] = {{"x3_256x128", 1}, {"x3_128x128", 0}, {"x3_dma", 2}, {"x3_128swz", 3}, {"x3_256swz", 4}, {"x3_256sq", 5}, {"x3_256sq_any", 6}, {"f32", -1}};
+    } vars[] = {{"x3_256swz", 4}, {"x3_128swz", 3}, {"x3_256sq", 5}, {"f32", -1}};
     std::vector<float> ref((size_t)M * N), out((size_t)M * N);
     for (auto& v : vars) {
       ConvGemmArgs q = g;
-      q.out = v.kind == 1 ? dref : dout;
+      q.out = v.kind == 4 ? dref : dout;
       auto launch = [&] {
         if (v.kind < 0) launch_conv_gemm(q, s);
-        else if (v.kind == 2) launch_conv_gemm_dma(q, dhi, dlo, s);
         else launch_conv_gemm_x3(q, dhi, dlo, v.kind, s);
       };
       try {
@@ -121,7 +120,7 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       ms /= reps;
       double diff = 0;
-      if (v.kind == 1) {
+      if (v.kind == 4) {
         CK(hipMemcpy(ref.data(), dref, ref.size() * 4, hipMemcpyDeviceToHost));
       } else {
         CK(hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost));

@@ -24,9 +24,8 @@ struct AstpArgs {
   const float* bias2;
   float var_floor;
   float* out;
-  int variant = 1;  // 1: 128 channels / 4 waves per block; 2: 256 / 8 waves, att chunks shared via LDS-DMA
 };
-bool astp_fused_supported(int C, int K, int variant = 1);
+bool astp_fused_supported(int C, int K);  // K = 128, C % 256 == 0
 void launch_astp_fused(const AstpArgs& p, hipStream_t s);
 
 }  // namespace wsp

@@ -6,7 +6,7 @@
 namespace wsp {
 
 // softmax(Q K^T / sqrt(dh)) V per (utterance, head); qkv [rows][ldq] = [q | k | v]
-// (H*dh each), out [rows][ldo].  Same contract as launch_mha (kernels.h).
+// (H*dh each), out [rows][ldo]; seg (device [B+1] row offsets) for ragged batches.
 void launch_attn(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s,
                  const int* seg = nullptr);
 

@@ -26,4 +26,26 @@ struct Conv3x3Args {
 bool conv3x3_img_supported(int C);
 void launch_conv3x3_img(const Conv3x3Args& p, int C, hipStream_t s);
 
+// Bottleneck tail in one launch (resnet.py:101-107, stride 1):
+//   y2  = relu(conv2_3x3(y1) + b2)                 (bn2 folded; never leaves the CU)
+//   out = relu(conv3_1x1(y2) + b3 + res)           (bn3 folded; res = x or the shortcut)
+// y1 [B][F][T][C], res / out [B][F][T][4C], NHWC fp32, C = planes in {32, 64, 128}.
+// w2 = conv3x3_img's fragment image of conv2.  w3 = [C/16 k-steps][hi, lo][4C/32 column
+// tiles][64 lanes][8] bf16 B fragments of conv3 whose lane l, element e holds
+// W3[n][16 ks + (e & 3) + 8 (e >> 2) + 4 (l >> 5)]: the k order in which conv2's
+// transposed accumulators hold y2's channels, so they feed conv3 as its A operand
+// straight from registers (Model::Impl::pack_frag_acc).
+struct BottleneckTailArgs {
+  const float* y1;
+  const float* res;
+  float* out;
+  int B, F, T;
+  const void* w2;
+  const float* b2;
+  const void* w3;
+  const float* b3;
+};
+bool bottleneck_tail_supported(int C);
+void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s);
+
 }  // namespace wsp

@@ -54,6 +54,43 @@ struct Img {
   __device__ __forceinline__ static int addr(int r, int ch) { return r * RB + ((ch ^ sw(r)) << 4); }
 };
 
+// The (f0 - 1 .. f0 + FB, t0 - 1 .. t0 + TB) input patch of utterance-relative
+// descriptor rx -> bf16 hi / lo image planes, zeros outside the utterance.
+template <typename G>
+__device__ __forceinline__ void stage_patch(__amdgpu_buffer_rsrc_t rx, int F, int T, int f0, int t0, int tid,
+                                            unsigned char* xhi, unsigned char* xlo) {
+  constexpr int C = G::RB / 2, PT = G::PT;
+  f32x4 v[G::NQ];
+#pragma unroll
+  for (int i = 0; i < G::NQ; ++i) {
+    const int q = tid + i * G::NT;
+    const int ir = q / G::C4;
+    const int c = (q - ir * G::C4) * 4;
+    const int pf = ir / PT;
+    const int f = f0 - 1 + pf, t = t0 - 1 + (ir - pf * PT);
+    const bool ok = q < G::IR * G::C4 && f >= 0 && f < F && t >= 0 && t < T;
+    v[i] = bload4(rx, ok ? ((f * T + t) * C + c) * 4 : kOOB);
+  }
+#pragma unroll
+  for (int i = 0; i < G::NQ; ++i) {
+    const int q = tid + i * G::NT;
+    if (q < G::IR * G::C4) {
+      const int ir = q / G::C4;
+      const int c = (q - ir * G::C4) * 4;
+      bf16x4 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const __bf16 hh = (__bf16)v[i][e];
+        hi[e] = hh;
+        lo[e] = (__bf16)(v[i][e] - (float)hh);
+      }
+      const int a = G::addr(ir, c >> 3) + (c & 7) * 2;
+      *reinterpret_cast<bf16x4*>(xhi + a) = hi;
+      *reinterpret_cast<bf16x4*>(xlo + a) = lo;
+    }
+  }
+}
+
 template <int C, int FB, int TB, int WN, int MINB, bool RES, bool RELU>
 __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void conv3x3_img_kernel(const Conv3x3Args p) {
   using G = Img<C, FB, TB, WN>;
@@ -77,37 +114,7 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void conv3x3_img_kernel(cons
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x + ubase);
 
   // ---- input patch (f0 - 1 .. f0 + FB, t0 - 1 .. t0 + TB) -> image, zeros outside
-  {
-    f32x4 v[G::NQ];
-#pragma unroll
-    for (int i = 0; i < G::NQ; ++i) {
-      const int q = tid + i * G::NT;
-      const int ir = q / G::C4;
-      const int c = (q - ir * G::C4) * 4;
-      const int pf = ir / PT;
-      const int f = f0 - 1 + pf, t = t0 - 1 + (ir - pf * PT);
-      const bool ok = q < G::IR * G::C4 && f >= 0 && f < p.F && t >= 0 && t < p.T;
-      v[i] = bload4(rx, ok ? ((f * p.T + t) * C + c) * 4 : kOOB);
-    }
-#pragma unroll
-    for (int i = 0; i < G::NQ; ++i) {
-      const int q = tid + i * G::NT;
-      if (q < G::IR * G::C4) {
-        const int ir = q / G::C4;
-        const int c = (q - ir * G::C4) * 4;
-        bf16x4 hi, lo;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const __bf16 hh = (__bf16)v[i][e];
-          hi[e] = hh;
-          lo[e] = (__bf16)(v[i][e] - (float)hh);
-        }
-        const int a = G::addr(ir, c >> 3) + (c & 7) * 2;
-        *reinterpret_cast<bf16x4*>(xhi + a) = hi;
-        *reinterpret_cast<bf16x4*>(xlo + a) = lo;
-      }
-    }
-  }
+  stage_patch<G>(rx, p.F, p.T, f0, t0, tid, xhi, xlo);
 
   // this lane's output position: patch-local (lf, lt); tap (kf, kt) reads image row
   // (lf + kf) * PT + lt + kt
@@ -196,6 +203,220 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void conv3x3_img_kernel(cons
   }
 }
 
+// Bottleneck tail (resnet.py:101-107, stride 1) in one launch:
+//   y2 = relu(conv2_3x3(y1) + b2),  out = relu(conv3_1x1(y2) + b3 + res)
+// Phase 1 is conv3x3_img's k-loop with the MFMA operands swapped (A = the W2
+// fragments, B = the image rows), so the accumulators hold y2 TRANSPOSED: lane l
+// = position l & 31 of the wave's run, register r of channel tile j = channel
+// 32 j + (r & 3) + 8 (r >> 2) + 4 (l >> 5).  That is an MFMA A-operand layout (row =
+// lane & 31, eight k slots per lane half) with the k slots permuted: after bias +
+// ReLU and the hi / lo split the registers ARE conv3's A fragments, and the
+// permutation is absorbed by packing W3's k in the same order (pack_frag_acc).
+// WN = 2 (C = 128): two waves share a 32-position run, each computing half of
+// conv2's channels (8 waves: two per SIMD); they swap their y2 fragments through
+// LDS (8 KB per wave, the image's space once conv2 is done) and each runs conv3 for
+// half of the 4C output columns over all C input channels.
+// Phase 2 runs conv3 over the wave's output columns in chunks of NC column tiles
+// (W3 fragments from L1 / L2 two k-steps ahead, the chunk's residual loaded before
+// its k-loop), then b3 + residual, ReLU, store.  y2 never exists in memory: per
+// position the HBM traffic is y1 (halo re-reads mostly L2 hits) + res + out instead
+// of conv2's y1 + y2 and conv3's y2 + res + out.
+template <int C, int FB, int TB, int WN, int MINB, int NC>
+__global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(const BottleneckTailArgs p) {
+  using G = Img<C, FB, TB, WN>;
+  constexpr int TN = G::TN, PT = G::PT;
+  constexpr int C4 = 4 * C, NT3 = C4 / 32, KS3 = C / 16;
+  constexpr int NTW = NT3 / WN, NCH = NTW / NC;  // conv3 column tiles per wave, chunks
+  static_assert(NTW % NC == 0 && KS3 % 2 == 0, "bottleneck_tail chunks");
+  static_assert(WN == 1 || G::IR * G::RB * 2 >= G::NW / WN * KS3 * 2048, "y2 exchange must fit the image");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* xhi = smem;
+  unsigned char* xlo = smem + G::PLANE;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+  const int ntf = (p.F + FB - 1) / FB, ntt = (p.T + TB - 1) / TB;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = id / (ntf * ntt);
+  const int rem = id - b * (ntf * ntt);
+  const int tf = rem / ntt;
+  const int f0 = tf * FB, t0 = (rem - tf * ntt) * TB;
+  const size_t plane = (size_t)p.F * p.T;
+  stage_patch<G>(make_rsrc(p.y1 + (size_t)b * plane * C), p.F, p.T, f0, t0, tid, xhi, xlo);
+
+  const int pr = wave / WN, wn = wave - pr * WN;  // position run, channel / column half
+  const int lf = pr / (TB / 32);
+  const int lt0 = (pr % (TB / 32)) * 32;
+  const int row0 = lf * PT + lt0 + r32;
+
+  // ---- phase 1: conv2 (this wave's TN channel tiles), transposed accumulators
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w2);
+  auto wload = [&](int g, bf16x8 (&bh)[TN], bf16x8 (&bl)[TN]) {
+    const bool ok = g < G::KS;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int o = ((g * 2 * G::CT + wn * TN + j) * 64 + lane) * 16;
+      bh[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? o : kOOB, 0, 0));
+      bl[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? o + G::CT * 1024 : kOOB, 0, 0));
+    }
+  };
+  auto read_b = [&](int g, bf16x8& xh, bf16x8& xl) {
+    const int tap = g / G::KC, cb = g - tap * G::KC;
+    const int kf = tap / 3, kt = tap - kf * 3;
+    const int a = G::addr(row0 + kf * PT + kt, 2 * cb + h);
+    xh = *reinterpret_cast<const bf16x8*>(xhi + a);
+    xl = *reinterpret_cast<const bf16x8*>(xlo + a);
+  };
+  f32x16 acc[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  auto mma_t = [&](const bf16x8& xh, const bf16x8& xl, const bf16x8 (&bh)[TN], const bf16x8 (&bl)[TN]) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], xl, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl[j], xh, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], xh, acc[j], 0, 0, 0);
+    }
+  };
+  {
+    bf16x8 b0h[TN], b0l[TN], b1h[TN], b1l[TN], x0h, x0l, x1h, x1l;
+    wload(0, b0h, b0l);
+    wload(1, b1h, b1l);
+    __syncthreads();  // image complete
+    read_b(0, x0h, x0l);
+#pragma unroll 1
+    for (int g = 0; g < G::KS; g += 2) {
+      read_b(g + 1, x1h, x1l);
+      mma_t(x0h, x0l, b0h, b0l);
+      wload(g + 2, b0h, b0l);
+      if (g + 2 < G::KS) read_b(g + 2, x0h, x0l);
+      mma_t(x1h, x1l, b1h, b1l);
+      wload(g + 3, b1h, b1l);
+    }
+  }
+
+  // ---- phase 2 operands: W3 fragments g = chunk * KS3 + ks of this wave's columns,
+  // the first two issued before the y2 conversion
+  const __amdgpu_buffer_rsrc_t rw3 = make_rsrc(p.w3);
+  auto w3load = [&](int g, bf16x8 (&bh)[NC], bf16x8 (&bl)[NC]) {
+    const bool ok = g < NCH * KS3;
+    const int ch = g / KS3, ks = g - ch * KS3;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int o = ((ks * 2 * NT3 + wn * NTW + ch * NC + j) * 64 + lane) * 16;
+      bh[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3, ok ? o : kOOB, 0, 0));
+      bl[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3, ok ? o + NT3 * 1024 : kOOB, 0, 0));
+    }
+  };
+  // slot q of the y2 fragments (below) holds conv3 k-step ksof(q): the wave's own k-steps
+  // first, then (WN = 2) the partner's
+  auto ksof = [&](int q) { return WN == 1 ? q : (q < 2 * TN ? wn * 2 * TN + q : (1 - wn) * 2 * TN + q - 2 * TN); };
+  bf16x8 c0h[NC], c0l[NC], c1h[NC], c1l[NC];
+  w3load(ksof(0), c0h, c0l);
+  w3load(ksof(1), c1h, c1l);
+
+  // ---- y2 = relu(acc + b2) -> conv3's A fragments (k-step 2 jj + s = registers 8 s .. 8 s + 7
+  // of channel tile jj = wn * TN + j)
+  bf16x8 yh[KS3], yl[KS3];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ch = 32 * (wn * TN + j) + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float y = fmaxf(acc[j][r] + p.b2[ch], 0.f);
+      const __bf16 hh = (__bf16)y;
+      // own k-steps sit at [0, 2 TN) of yh / yl; the partner's (WN = 2) at [2 TN, 4 TN)
+      yh[2 * j + (r >> 3)][r & 7] = hh;
+      yl[2 * j + (r >> 3)][r & 7] = (__bf16)(y - (float)hh);
+    }
+  if constexpr (WN == 2) {
+    // swap halves with the partner wave through LDS: [run][k-step][plane][64 lanes] x 16 B
+    __syncthreads();  // every wave is done reading the image
+#pragma unroll
+    for (int q = 0; q < 2 * TN; ++q) {
+      const int o = ((pr * KS3 + ksof(q)) * 2) * 1024 + lane * 16;
+      *reinterpret_cast<bf16x8*>(smem + o) = yh[q];
+      *reinterpret_cast<bf16x8*>(smem + o + 1024) = yl[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 2 * TN; q < KS3; ++q) {
+      const int o = ((pr * KS3 + ksof(q)) * 2) * 1024 + lane * 16;
+      yh[q] = *reinterpret_cast<const bf16x8*>(smem + o);
+      yl[q] = *reinterpret_cast<const bf16x8*>(smem + o + 1024);
+    }
+  }
+
+  // ---- phase 2: conv3 over NCH chunks of NC column tiles
+  const size_t obase = (size_t)b * plane * C4;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out + obase);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res + obase);
+  const int f = f0 + lf;
+  const int tw = t0 + lt0 + 4 * h;  // time of register 0
+  auto roff = [&](int col, int r) {
+    const int t = tw + (r & 3) + 8 * (r >> 2);
+    return f < p.F && t < p.T ? ((f * p.T + t) * C4 + col) * 4 : kOOB;
+  };
+#pragma unroll 1
+  for (int chunk = 0; chunk < NCH; ++chunk) {
+    const int cb = (wn * NTW + chunk * NC) * 32 + r32;  // column of tile 0
+    float rv[NC][16];
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        rv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, roff(cb + 32 * j, r), 0, 0));
+    f32x16 a3[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a3[j][r] = 0.f;
+    // slots in k order: k-step ks lives in slot q with ksof(q) == ks; summing in slot order
+    // is the same sum (the fp32 accumulation order differs from k order only by whole k-steps)
+#pragma unroll
+    for (int q = 0; q < KS3; q += 2) {
+      // W3 fragments were loaded for k-steps ksof(q), ksof(q + 1) (consecutive: own / partner
+      // halves are each 2 TN consecutive k-steps and 2 TN is even)
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        a3[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yl[q], c0h[j], a3[j], 0, 0, 0);
+        a3[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yh[q], c0l[j], a3[j], 0, 0, 0);
+        a3[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yh[q], c0h[j], a3[j], 0, 0, 0);
+      }
+      {
+        const int qn = q + 2 < KS3 ? q + 2 : 0;
+        w3load((q + 2 < KS3 ? chunk : chunk + 1) * KS3 + ksof(qn), c0h, c0l);
+      }
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        a3[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yl[q + 1], c1h[j], a3[j], 0, 0, 0);
+        a3[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yh[q + 1], c1l[j], a3[j], 0, 0, 0);
+        a3[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yh[q + 1], c1h[j], a3[j], 0, 0, 0);
+      }
+      {
+        const int qn = q + 3 < KS3 ? q + 3 : 1;
+        w3load((q + 3 < KS3 ? chunk : chunk + 1) * KS3 + ksof(qn), c1h, c1l);
+      }
+    }
+    // epilogue: y = relu(acc + b3 + res), conv3x3_img's store pattern over 4C channels
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int col = cb + 32 * j;
+      const float bv = p.b3[col];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float y = fmaxf(a3[j][r] + bv + rv[j][r], 0.f);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, roff(col, r), 0, 0);
+      }
+    }
+  }
+}
+
 template <int C, int FB, int TB, int MINB, int WN = 1>
 void launch_k(const Conv3x3Args& p, hipStream_t s) {
   using G = Img<C, FB, TB, WN>;
@@ -226,6 +447,33 @@ void launch_conv3x3_img(const Conv3x3Args& p, int C, hipStream_t s) {
     launch_k<128, 4, 32, 1, 2>(p, s);  // 128 positions, 8 waves x 2 column tiles, 102 KB image
   else
     launch_k<128, 4, 32, 1>(p, s);  // 128 positions, 4 waves x 4 column tiles, 102 KB image
+  WSP_HIP(hipGetLastError());
+}
+
+namespace {
+template <int C, int FB, int TB, int WN, int MINB, int NC>
+void launch_tail_k(const BottleneckTailArgs& p, hipStream_t s) {
+  using G = Img<C, FB, TB, WN>;
+  const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + TB - 1) / TB);
+  hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB, NC>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
+}
+}  // namespace
+
+bool bottleneck_tail_supported(int C) { return C == 32 || C == 64 || C == 128; }
+
+void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s) {
+  WSP_CHECK(bottleneck_tail_supported(C), "bottleneck_tail: planes must be 32, 64 or 128");
+  WSP_CHECK(p.B > 0 && p.F > 0 && p.T > 0 && p.y1 && p.res && p.out && p.w2 && p.w3 && p.b2 && p.b3,
+            "bottleneck_tail: bad arguments");
+  WSP_CHECK(p.out != p.res && p.out != p.y1, "bottleneck_tail: out must not alias its inputs");
+  // buffer offsets are per utterance (descriptors based at its first element)
+  WSP_CHECK((long long)p.F * p.T * 4 * C * 4 < (long long)kOOB, "bottleneck_tail: utterance exceeds 2 GiB");
+  if (C == 32)
+    launch_tail_k<32, 4, 64, 1, 4, 1>(p, s);  // 256 positions, 8 waves, 50 KB image: 2 blocks / CU
+  else if (C == 64)
+    launch_tail_k<64, 4, 32, 1, 3, 2>(p, s);  // 128 positions, 4 waves, 51 KB image: 3 blocks / CU
+  else
+    launch_tail_k<128, 4, 32, 2, 2, 2>(p, s);  // 128 positions, 8 waves (2 per position run), 102 KB image
   WSP_HIP(hipGetLastError());
 }
 

@@ -25,7 +25,7 @@ namespace wsp {
 int conv_gemm_x3_block_rows(const ConvGemmArgs& p, int variant) {
   if (p.N % 64 != 0 || (p.gcols && p.gcols % 64 != 0)) return 128;
   if (p.gcols || p.N % 128 != 0) return 128;
-  return (variant == 1 || variant == 4 || variant == 5 || variant == 6) ? 256 : 128;
+  return variant == 3 ? 128 : 256;
 }
 
 namespace {
@@ -58,11 +58,11 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
   check_conv_args(p, "conv_gemm_x3");
   if (p.colsum) {
     const int bm = conv_gemm_x3_block_rows(p, variant);
-    WSP_CHECK(!p.seg && !p.row_bias && !p.conv2d && p.T >= bm && (variant == 1 || variant == 3 || variant == 4 ||
-                                                                  variant == 5 || variant == 6 || variant == 0),
+    WSP_CHECK(!p.seg && !p.row_bias && !p.conv2d && p.T >= bm,
               "conv_gemm_x3: column sums need a uniform batch with T >= block rows and no row bias");
   }
   WSP_CHECK(p.Kp % 64 == 0, "conv_gemm_x3: packed K must be a multiple of 64");
+  WSP_CHECK(variant == 3 || variant == 4 || variant == 5, "conv_gemm_x3: tile family must be 3, 4 or 5");
   const __bf16* h = static_cast<const __bf16*>(whi);
   const __bf16* l = static_cast<const __bf16*>(wlo);
   x3::TileFn f;
@@ -74,23 +74,17 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
     f = variant == 5 ? x3::t_8x1_1x2_sw : x3::t_4x1_1x2;  // blocks stay inside one group
   } else if (p.N % 128 != 0) {
     f = x3::t_4x1_1x2;  // 128 x 64, 4 waves
-  } else if (variant == 1) {
-    f = x3::t_4x2_2x2;  // 256 x 128, 8 waves
   } else if (variant == 3) {
     f = x3::t_2x2_2x2_sw;  // 128 x 128, 4 waves, swizzled rows: 2 blocks / CU
   } else if (variant == 4) {
     f = x3::t_4x2_2x2_sw;  // 256 x 128, 8 waves, swizzled rows
-  } else if (variant == 5 || variant == 6) {
-    // 256 x 256 (8 waves 4 x 2, 64 x 128 per wave) wherever N allows it: in-model C x C
-    // -10 %, conv_cat -15 %, HuBERT fc1 -18 %, fc2 -20 %, CNN -12 % vs 256 x 128 (with the
-    // per-tile residual epilogue and the A&S GELU; the libm erff made fc1's epilogue lose).
-    // (Variant 6 = 5: the former experiments slot.)
-    if (p.N % 256 == 0)
-      f = x3::t_4x2_2x4_sw1;
-    else
-      f = x3::t_4x2_2x2_sw;  // variant 4
+  } else if (p.N % 256 == 0) {
+    // variant 5: 256 x 256 (8 waves 4 x 2, 64 x 128 per wave) wherever N allows it: in-model
+    // C x C -10 %, conv_cat -15 %, HuBERT fc1 -18 %, fc2 -20 %, CNN -12 % vs 256 x 128 (with
+    // the per-tile residual epilogue and the A&S GELU; the libm erff made fc1's epilogue lose).
+    f = x3::t_4x2_2x4_sw1;
   } else {
-    f = x3::t_2x2_2x2;  // 128 x 128, 4 waves
+    f = x3::t_4x2_2x2_sw;  // variant 5 with N % 256 != 0
   }
   f(p, h, l, s);
 }

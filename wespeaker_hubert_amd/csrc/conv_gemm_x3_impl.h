@@ -282,8 +282,6 @@ using TileFn = void (*)(const ConvGemmArgs&, const __bf16*, const __bf16*, hipSt
 void t_4x1_1x1(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);      // 128 x 32
 void t_4x1_1x2(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);      // 128 x 64
 void t_8x1_1x2_sw(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);   // 256 x 64 swizzled
-void t_4x2_2x2(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);      // 256 x 128 (v1)
-void t_2x2_2x2(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);      // 128 x 128 (v0)
 void t_2x2_2x2_sw(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);   // 128 x 128 swizzled (v3)
 void t_4x2_2x2_sw(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);   // 256 x 128 swizzled (v4)
 void t_4x2_2x4_sw1(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);  // 256 x 256, one set (v5)

@@ -362,8 +362,6 @@ __device__ __forceinline__ void gemm_colsum_reduce(const ConvGemmArgs& p, double
 template <int TM, int TN, int WM = 0, int WN = 0>
 __device__ __forceinline__ void gemm_epilogue(const ConvGemmArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0,
                                               int wm, int wn, int lane, unsigned char* smem = nullptr) {
-  const int r32 = lane & 31;
-  const int h = lane >> 5;
   if constexpr (WM > 0) {
     if (p.colsum) {  // fused per-utterance column sums (host: uniform batch, T >= BM, no row bias)
       double cs[TN][2];

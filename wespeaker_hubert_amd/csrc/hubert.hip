@@ -1,15 +1,14 @@
 // HuBERT-base front-end kernels (s3prl `hubert` upstream as wrapped by
 // wespeaker/frontend/s3prl.py:23-93; fairseq HuBERT semantics, restated in
 // oracle/hubert_ref.py).  The dense contractions (conv1..6, projections, FFN,
-// pos_conv) run on the implicit-GEMM MFMA kernels; this file holds the rest:
+// pos_conv) run on the implicit-GEMM MFMA kernels and self-attention on attn.hip;
+// this file holds the rest:
 //
 //   conv0 + GroupNorm(512, 512) + GELU : waveform -> [B][T0][512]
 //       (1 input channel, k10 s5: 10 MACs per output — VALU, recomputed per
 //        pass instead of round-tripping 33 MB/utt of pre-norm activations)
 //   layernorm  : rows of D in {512, 768}, optional (remapped) residual add,
 //                optional s3prl Featurizer accumulation + length match
-//   mha        : softmax(QK^T/8) V per (utterance, head) on bf16x3 MFMA, online
-//                softmax over 32-key chunks staged in LDS (T = 249 frames for 5 s)
 //   cmn_rows   : per-utterance mean removal over frames (dataset_utils.py:19-26)
 #include <cfloat>
 
@@ -166,174 +165,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LayerNormArgs p) {
   }
 }
 
-// ------------------------------------------------------------------ mha ---
-// softmax(Q K^T / 8) V on bf16x3 MFMA (fp32-class: every product is
-// a_hi*b_hi + a_hi*b_lo + a_lo*b_hi with fp32 accumulation).
-// Block = (128 queries, head, utterance), 4 waves x 32 queries; keys stream in
-// 32-key chunks through a double-buffered LDS ring (K as [key][d], V as
-// V^T [d][key]), the next chunk's global loads in flight during the current
-// chunk's MFMAs.  Per chunk each wave computes S^T = K_c Q^T (32 keys x 32
-// queries: query on the lane, keys in the accumulator registers), an online
-// softmax per lane-column, then O^T += V_c^T P with P taken straight from the
-// S^T accumulator registers (cdna_hip_programming.md §3: an accumulator tile
-// as the next MFMA's B operand, k order 16s + 8(j>>2) + 4h + (j&3)).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-constexpr int kDH = 64, kQW = 32, kWaves = 4, kKC = 32;
-constexpr int kKLD = kDH + 4;  // Ks row stride (floats): conflict-free ds_read_b128 over 32 key rows
-constexpr int kVLD = kKC + 4;  // VTs row stride (floats)
-
-__device__ __forceinline__ void split8(const f32x4 a, const f32x4 b, bf16x8& hi, bf16x8& lo) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const __bf16 h0 = (__bf16)a[e], h1 = (__bf16)b[e];
-    hi[e] = h0;
-    hi[e + 4] = h1;
-    lo[e] = (__bf16)(a[e] - (float)h0);
-    lo[e + 4] = (__bf16)(b[e] - (float)h1);
-  }
-}
-
-__device__ __forceinline__ f32x16 mma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
-                                       f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
-}
-
-__global__ __launch_bounds__(256) void mha_kernel(const float* __restrict__ qkv, int ldq, float* __restrict__ out,
-                                                  int ldo, int T_, int D, float scale, const int* __restrict__ seg) {
-  __shared__ __attribute__((aligned(16))) float Ks[2][kKC * kKLD];
-  __shared__ __attribute__((aligned(16))) float VTs[2][kDH * kVLD];
-  const int b = blockIdx.z, head = blockIdx.y;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int q = blockIdx.x * (kQW * kWaves) + wave * kQW + r;
-  // segmented batch: utterance b = rows [seg[b], seg[b+1]); attention stays inside it
-  const size_t rbase = seg ? (size_t)seg[b] : (size_t)b * T_;
-  const int T = seg ? seg[b + 1] - seg[b] : T_;
-  if (blockIdx.x * (kQW * kWaves) >= T) return;  // block-uniform
-  const float* base = qkv + rbase * ldq;
-  const float* kbase = base + D + head * kDH;
-  const float* vbase = base + 2 * D + head * kDH;
-
-  // Q^T fragments (B operand of S^T = K Q^T): lane = query r, d = 16s + 8hh + j; pre-scaled by
-  // 1/sqrt(dh) = 1/8 (exact in binary).
-  bf16x8 qh[4], ql[4];
-  {
-    const float* qr = base + (size_t)min(q, T - 1) * ldq + head * kDH + 8 * hh;
-    const float sc = q < T ? scale : 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(qr + 16 * s) * sc;
-      const f32x4 c = *reinterpret_cast<const f32x4*>(qr + 16 * s + 4) * sc;
-      split8(a, c, qh[s], ql[s]);
-    }
-  }
-
-  // chunk staging: 2 float4 of K and 2 of V per thread (32 keys x 64 d each)
-  f32x4 kr[2], vr[2];
-  auto load_chunk = [&](int c) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int f = tid + 256 * i, key = c * kKC + (f >> 4), d4 = (f & 15) * 4;
-      const bool ok = key < T;
-      const size_t off = (size_t)(ok ? key : 0) * ldq + d4;
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      kr[i] = ok ? *reinterpret_cast<const f32x4*>(kbase + off) : z;
-      vr[i] = ok ? *reinterpret_cast<const f32x4*>(vbase + off) : z;
-    }
-  };
-  auto store_chunk = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int f = tid + 256 * i, key = f >> 4, d4 = (f & 15) * 4;
-      *reinterpret_cast<f32x4*>(&Ks[buf][key * kKLD + d4]) = kr[i];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) VTs[buf][(d4 + e) * kVLD + key] = vr[i][e];
-    }
-  };
-
-  f32x16 o[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) o[t][e] = 0.f;
-  float m = -FLT_MAX, l = 0.f;
-
-  const int nch = (T + kKC - 1) / kKC;
-  load_chunk(0);
-  store_chunk(0);
-  __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < nch) load_chunk(c + 1);
-    // S^T (32 keys x 32 queries)
-    f32x16 st;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) st[e] = 0.f;
-    const float* kp = &Ks[buf][r * kKLD + 8 * hh];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 kh, kl;
-      split8(*reinterpret_cast<const f32x4*>(kp + 16 * s), *reinterpret_cast<const f32x4*>(kp + 16 * s + 4), kh, kl);
-      st = mma3(kh, kl, qh[s], ql[s], st);
-    }
-    // online softmax over the keys of this lane's query column
-    float cmax = -FLT_MAX;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int key = c * kKC + (e & 3) + 8 * (e >> 2) + 4 * hh;
-      if (key >= T) st[e] = -FLT_MAX;
-      cmax = fmaxf(cmax, st[e]);
-    }
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-    const float mn = fmaxf(m, cmax);
-    const float corr = expf(m - mn);
-    float ls = 0.f;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int key = c * kKC + (e & 3) + 8 * (e >> 2) + 4 * hh;
-      const float pe = key < T ? expf(st[e] - mn) : 0.f;
-      st[e] = pe;
-      ls += pe;
-    }
-    l = l * corr + ls;
-    m = mn;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) o[t][e] *= corr;
-    // O^T (64 d x 32 queries) += V_c^T P
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 ph, pl;
-      const f32x4 p0 = {st[8 * s], st[8 * s + 1], st[8 * s + 2], st[8 * s + 3]};
-      const f32x4 p1 = {st[8 * s + 4], st[8 * s + 5], st[8 * s + 6], st[8 * s + 7]};
-      split8(p0, p1, ph, pl);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const float* vp = &VTs[buf][(32 * t + r) * kVLD + 16 * s + 4 * hh];
-        bf16x8 vh, vl;
-        split8(*reinterpret_cast<const f32x4*>(vp), *reinterpret_cast<const f32x4*>(vp + 8), vh, vl);
-        o[t] = mma3(vh, vl, ph, pl, o[t]);
-      }
-    }
-    if (c + 1 < nch) store_chunk(buf ^ 1);
-    __syncthreads();
-  }
-  const float inv = 1.f / (l + __shfl_xor(l, 32, 64));
-  if (q < T) {
-    float* op = out + (rbase + q) * ldo + head * kDH + 4 * hh;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 v = {o[t][4 * g] * inv, o[t][4 * g + 1] * inv, o[t][4 * g + 2] * inv, o[t][4 * g + 3] * inv};
-        *reinterpret_cast<f32x4*>(op + 32 * t + 8 * g) = v;
-      }
-  }
-}
-
 // ------------------------------------------------------------- cmn_rows ---
 // Block = (64 channels, utterance); 4 row groups of 64 lanes: coalesced
 // 256-B row segments, partial sums combined through LDS.
@@ -388,16 +219,6 @@ void launch_layernorm(const LayerNormArgs& p, hipStream_t s) {
     hipLaunchKernelGGL(layernorm_kernel<2>, grid, dim3(256), 0, s, p);
   else
     hipLaunchKernelGGL(layernorm_kernel<3>, grid, dim3(256), 0, s, p);
-  WSP_HIP(hipGetLastError());
-}
-
-void launch_mha(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s,
-                const int* seg) {
-  WSP_CHECK(dh == kDH, "mha: head dim must be 64");
-  WSP_CHECK(B > 0 && T > 0 && H > 0 && ldq >= 3 * H * dh && ldq % 4 == 0 && ldo % 4 == 0, "mha: bad shape");
-  const dim3 grid((T + kQW * kWaves - 1) / (kQW * kWaves), H, B);  // segmented: T = longest utterance
-  hipLaunchKernelGGL(mha_kernel, grid, dim3(256), 0, s, qkv, ldq, out, ldo, T, H * dh, 1.f / sqrtf((float)dh),
-                     seg);
   WSP_HIP(hipGetLastError());
 }
 

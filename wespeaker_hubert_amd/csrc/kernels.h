@@ -76,9 +76,9 @@ inline ConvGemmArgs normalized(ConvGemmArgs p) {
 }
 
 // bf16x3 split-precision variant (conv_gemm_x3.hip); whi/wlo = packed [N][Kp]
-// bf16 hi/lo images of W.  variant (N % 128 == 0): 0 = 128x128/4 waves,
-// 1 = 256x128/8 waves, 3 = 128x128 swizzled LDS rows (2 blocks/CU),
-// 4 = 256x128 swizzled LDS rows (default).
+// bf16 hi/lo images of W.  variant (N % 128 == 0): 3 = 128x128 / 4 waves,
+// 4 = 256x128 / 8 waves, 5 = 256x256 / 8 waves where N % 256 == 0 (else 4);
+// all with XOR-swizzled LDS rows.
 // Rows per block of the bf16x3 tile launch_conv_gemm_x3 picks for p / variant
 // (the colsum partials' granularity).
 int conv_gemm_x3_block_rows(const ConvGemmArgs& p, int variant);
@@ -89,9 +89,6 @@ void launch_colsum_mean(const double* part, int block_rows, int T, int B, int N,
 void launch_conv_gemm_x3(const ConvGemmArgs& p, const void* whi, const void* wlo, int variant,
                          hipStream_t s);
 
-// LDS-DMA staged bf16x3 variant (conv_gemm_dma.hip): kACat operands, N % 128.
-bool conv_gemm_dma_supported(const ConvGemmArgs& p);
-void launch_conv_gemm_dma(const ConvGemmArgs& p, const void* whi, const void* wlo, hipStream_t s);
 
 // tile: 0 = 128x128 block (N % 128 == 0), 1 = 128x64 block (N % 64 == 0)
 void launch_conv_gemm(const ConvGemmArgs& p, hipStream_t s);
@@ -188,9 +185,6 @@ struct LayerNormArgs {
   int nseg;
 };
 void launch_layernorm(const LayerNormArgs& p, hipStream_t s);
-// softmax(Q K^T / sqrt(dh)) V per (utterance, head); qkv [B*T][ldq] = [q | k | v] (H*dh each).
-void launch_mha(const float* qkv, int ldq, float* out, int ldo, int B, int T, int H, int dh, hipStream_t s,
-                const int* seg = nullptr);
 // x [B][T][D] -= mean over T  (apply_cmvn(norm_mean=True, norm_var=False))
 void launch_cmn_rows(float* x, int B, int T, int D, hipStream_t s, const int* seg = nullptr);
 

@@ -225,23 +225,20 @@ void Model::set_option(const std::string& key, int value) {
     for (const auto& p : impl->params) WSP_CHECK(!p.set, "option 'in_planes' must be set before the weights");
     impl->m_ch = value;
     impl->build_simam_params();
-  } else if (key == "conv1x1_rows") {
-    WSP_CHECK(value == 0 || value == 1, "conv1x1_rows must be 0 or 1");
-    impl->conv1x1_rows_on = value;
   } else if (key == "res_prefetch") {
     WSP_CHECK(value == 0 || value == 1, "res_prefetch must be 0 or 1");
     impl->res_prefetch = value;
+  } else if (key == "res_tail") {
+    WSP_CHECK(value == 0 || value == 1, "res_tail must be 0 or 1");
+    impl->res_tail = value;
   } else if (key == "cat_gate") {
     WSP_CHECK(value == 0 || value == 1, "cat_gate must be 0 or 1");
     impl->cat_gate = value;
   } else if (key == "res2_fused") {
     WSP_CHECK(value == 0 || value == 1, "res2_fused must be 0 or 1");
     impl->res2_fused = value;
-  } else if (key == "attn_lds") {
-    WSP_CHECK(value == 0 || value == 1, "attn_lds must be 0 or 1");
-    impl->attn_lds = value;
   } else if (key == "astp_fused") {
-    WSP_CHECK(value >= 0 && value <= 3, "astp_fused must be 0 (unfused) or 1..3 (fused kernel variant)");
+    WSP_CHECK(value == 0 || value == 1, "astp_fused must be 0 (linear2 GEMM + pooling kernel) or 1 (fused)");
     impl->astp_fused_on = value;
   } else if (key == "conv3x3_img") {
     WSP_CHECK(value >= 0 && value <= 3, "conv3x3_img must be 0 (off), 1 (32 / 64 channels) or 2 / 3 (also 128)");
@@ -250,9 +247,10 @@ void Model::set_option(const std::string& key, int value) {
     WSP_CHECK(value >= 1 && value <= 8, "streams must be 1..8");
     impl->streams = value;
   } else if (key == "res2_variant") {
+    WSP_CHECK(value >= 0 && value <= 2, "res2_variant must be 0 (128 rows), 1 (256 rows) or 2 (128 rows, 4 waves on N)");
     impl->res2_variant = value;
   } else if (key == "x3_variant") {
-    WSP_CHECK((value >= 0 && value <= 6) || value == 9, "x3_variant must be 0..6 or 9");
+    WSP_CHECK(value == 3 || value == 4 || value == 5, "x3_variant must be 3, 4 or 5");
     impl->x3_variant = value;
   } else {
     throw InvalidArg{"unknown option " + key};
@@ -268,8 +266,7 @@ int Model::get_option(const std::string& key) const {
   if (key == "res2_fused") return m.res2_fused;
   if (key == "cat_gate") return m.cat_gate;
   if (key == "res_prefetch") return m.res_prefetch;
-  if (key == "conv1x1_rows") return m.conv1x1_rows_on;
-  if (key == "attn_lds") return m.attn_lds;
+  if (key == "res_tail") return m.res_tail;
   if (key == "astp_fused") return m.astp_fused_on;
   if (key == "res2_variant") return m.res2_variant;
   if (key == "x3_variant") return m.x3_variant;

@@ -16,9 +16,7 @@
 #include "kernels.h"
 #include "model.h"
 #include "res2_chain.h"
-#include "gemm_dma.h"
 #include "astp_fused.h"
-#include "conv1x1_rows.h"
 #include "conv3x3_img.h"
 
 namespace wsp {
@@ -56,7 +54,7 @@ struct ConvW {
   float* scale = nullptr;
   float* shift = nullptr;
   int N = 0, cin = 0, taps = 1, K = 0, Kp = 0;
-  void* frag = nullptr;  // MFMA B-fragment order: 3x3 N = cin (conv3x3_img.hip), 1x1 (conv1x1_rows.hip)
+  void* frag = nullptr;  // MFMA B-fragment order of a stride-1 3x3 conv with N = cin (conv3x3_img.hip)
 };
 
 struct LinW {  // small_linear weights, k-major
@@ -146,8 +144,10 @@ struct Model::Impl {
   // ResNet stride-1 3x3 convs on conv3x3_img.hip (option "conv3x3_img"): 0 = off (implicit GEMM),
   // 1 = 32 / 64 channels, 2 = also 128 channels (4 x 32 tile), 3 = also 128 (2 x 32 tile)
   int conv3x3_img_on = 2;
-  int conv1x1_rows_on = 0;  // ResNet conv1 (1x1 K -> K/4) on conv1x1_rows.hip (option "conv1x1_rows")
   int res_prefetch = 1;  // ResNet 1x1 residual convs: residual loaded ahead of the last k-tiles (option "res_prefetch")
+  // ResNet bottleneck conv2 + conv3 (+ residual) of stride-1 blocks with planes 32 / 64 / 128 in one
+  // launch, y2 kept in registers (conv3x3_img.hip bottleneck_tail; option "res_tail")
+  int res_tail = 1;
   bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
   int res2_variant = 0;  // res2_chain.hip kernel variant (option "res2_variant")
   ConvW conv, pool1, pool2;
@@ -157,9 +157,9 @@ struct Model::Impl {
   ConvW conv_g;
   int cat_gate = 1;
   void* pool2_frag = nullptr;  // pool.linear2 in MFMA B-fragment order for astp_fused.hip
-  // 0: linear2 GEMM + separate pooling kernel; 1..3: astp_fused.hip variant (option "astp_fused";
-  // 3 = 256 channels per block, att chunks two ahead in an LDS-DMA ring, W2 in VGPRs: C2 0.465 -> 0.31 ms)
-  int astp_fused_on = 3;
+  // 0: linear2 GEMM + separate pooling kernel; 1: astp_fused.hip (option "astp_fused"; 256 channels
+  // per block, att chunks two ahead in an LDS-DMA ring, W2 in VGPRs: C2 0.465 -> 0.31 ms)
+  int astp_fused_on = 1;
   LinW pool1_ctx;
   LinW head;
 
@@ -171,6 +171,7 @@ struct Model::Impl {
   float* stem_b = nullptr;
   struct RBlock {
     ConvW c1, c2, c3, sc;
+    void* w3acc = nullptr;  // conv3 (bn3 folded) as pack_frag_acc B fragments for bottleneck_tail
     bool has_sc = false;
     int stride = 1, in_planes = 0, planes = 0, out_planes = 0;
   };
@@ -201,7 +202,6 @@ struct Model::Impl {
   std::vector<HLayer> h_layers;
   std::vector<float> h_fw;  // featurizer weight per hidden state
   int h_layer_sel = -1;     // s3prl `layer` (-1: softmax-weighted sum of all 13)
-  int attn_lds = 1;         // 1: attn.hip (K / V staged once in LDS), 0: hubert.hip mha_kernel (option "attn_lds")
   void build_hubert_params();
   void finalize_hubert();
   int hubert_cnn_frames(int N, int upto) const;
@@ -215,9 +215,9 @@ struct Model::Impl {
 
   // 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA
   int precision = 1;
-  int x3_variant = 5;  // 256 x 256 bf16x3 tiles where N % 256 == 0, else 256 x 128 (tools/gemm_bench)
-  // conv_gemm_x3 variant behind x3_variant (the DMA selections 2 / 9 fall back to 5)
-  int x3_base() const { return (x3_variant == 2 || x3_variant >= 7) ? 5 : x3_variant; }
+  // bf16x3 tile family (conv_gemm_x3.hip): 5 = 256 x 256 where N % 256 == 0, else 256 x 128;
+  // 4 = 256 x 128; 3 = 128 x 128 (option "x3_variant")
+  int x3_variant = 5;
 
   // concurrent sub-batches (option "streams"): the batch's utterances are split
   // into `streams` contiguous ranges, each forwarded on its own HIP stream over its
@@ -345,6 +345,27 @@ struct Model::Impl {
     return dev.upload_u16(pk);
   }
 
+  // As pack_frag, but lane l, element e of k-step ks holds k = 16 ks + (e & 3) + 8 (e >> 2)
+  // + 4 (l >> 5): the order in which a transposed 32x32 accumulator tile holds its 32 rows
+  // (register r = (r & 3) + 8 (r >> 2) + 4 (l >> 5)), so such accumulators feed this
+  // weight's MFMAs as the A operand without a shuffle (bottleneck_tail).
+  void* pack_frag_acc(const std::vector<float>& w, int N, int K) {
+    const int KS = K / 16, NT = N / 32;
+    std::vector<uint16_t> pk((size_t)KS * 2 * NT * 64 * 8);
+    for (int ks = 0; ks < KS; ++ks)
+      for (int jt = 0; jt < NT; ++jt)
+        for (int l = 0; l < 64; ++l)
+          for (int e = 0; e < 8; ++e) {
+            const int k = ks * 16 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+            const float v = w[(size_t)(jt * 32 + (l & 31)) * K + k];
+            const uint16_t hi = f2bf(v), lo = f2bf(v - bf2f(hi));
+            const size_t o = (((size_t)ks * 2 * NT + jt) * 64 + l) * 8 + e;
+            pk[o] = hi;
+            pk[o + (size_t)NT * 64 * 8] = lo;
+          }
+    return dev.upload_u16(pk);
+  }
+
   // Linear weight [N][K] (row-major, ldk) -> k-major [K][N]
   LinW pack_lin(const float* w, int N, int K, int ldk, const float* bias) {
     LinW lw;
@@ -443,7 +464,8 @@ struct Model::Impl {
   }
 
   // conv -> BN (eval) folded into the weights: W' = W * s[n], bias = shift.
-  ConvW pack_conv_bn(const std::string& wname, const std::string& bn, int N, int cin, int taps) {
+  ConvW pack_conv_bn(const std::string& wname, const std::string& bn, int N, int cin, int taps,
+                     void** acc_frag = nullptr) {
     std::vector<double> sc, sh;
     bn_affine(bn, sc, sh);
     std::vector<float> w = P(wname);
@@ -452,7 +474,7 @@ struct Model::Impl {
     std::vector<float> b(N);
     for (int n = 0; n < N; ++n) b[n] = (float)sh[n];
     ConvW cw = pack_conv(w, N, cin, taps, b.data(), "");
-    if (taps == 1 && conv1x1_rows_supported(cin, N)) cw.frag = pack_frag(w, N, cin);  // k = c
+    if (acc_frag) *acc_frag = pack_frag_acc(w, N, cin * taps);
     if (taps == 9 && N == cin && conv3x3_img_supported(cin)) {
       // the same k = tap * cin + c order as the implicit GEMM's packed image
       std::vector<float> wk((size_t)N * 9 * cin);
@@ -485,7 +507,8 @@ struct Model::Impl {
         if (bottleneck) {
           rb.c1 = pack_conv_bn(p + ".conv1.weight", p + ".bn1", rb.planes, rb.in_planes, 1);
           rb.c2 = pack_conv_bn(p + ".conv2.weight", p + ".bn2", rb.planes, rb.planes, 9);
-          rb.c3 = pack_conv_bn(p + ".conv3.weight", p + ".bn3", rb.out_planes, rb.planes, 1);
+          rb.c3 = pack_conv_bn(p + ".conv3.weight", p + ".bn3", rb.out_planes, rb.planes, 1,
+                               rb.stride == 1 && bottleneck_tail_supported(rb.planes) ? &rb.w3acc : nullptr);
         } else {
           rb.c1 = pack_conv_bn(p + ".conv1.weight", p + ".bn1", rb.planes, rb.in_planes, 9);
           rb.c2 = pack_conv_bn(p + ".conv2.weight", p + ".bn2", rb.planes, rb.planes, 9);
@@ -590,7 +613,7 @@ struct Model::Impl {
     g.kw = kw;
     g.res = res;
     g.ldres = ldres;
-    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_base(), s); });
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant, s); });
   }
   void gemm1x1(const char* tag, const ConvW& cw, const float* a0, float* out, int M, int act, const float* res,
                hipStream_t s) {
@@ -603,13 +626,7 @@ struct Model::Impl {
     g.res = res;
     g.ldres = cw.N;
     g.role = res && res_prefetch ? 2 : 0;
-    if (!res && act == kActRelu && cw.frag && cw.taps == 1 && conv1x1_rows_on) {
-      // whole rows staged in LDS (conv1x1_rows.hip): bit-identical to the GEMM below
-      const Conv1x1Args a{a0, out, M, cw.frag, cw.bias, cw.scale, cw.shift, 1};
-      run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv1x1_rows(a, cw.cin, cw.N, s); });
-      return;
-    }
-    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_base(), s); });
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant, s); });
   }
 
   void forward_resnet(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
@@ -636,6 +653,7 @@ struct Model::Impl {
       static const char* kC3[4] = {"res_conv1x1.c3.L1", "res_conv1x1.c3.L2", "res_conv1x1.c3.L3",
                                    "res_conv1x1.c3.L4"};
       static const char* kK3[4] = {"res_conv3x3.L1", "res_conv3x3.L2", "res_conv3x3.L3", "res_conv3x3.L4"};
+      static const char* kTl[4] = {"res_tail.L1", "res_tail.L2", "res_tail.L3", "res_tail.L4"};
       int ib = 0;
       for (const RBlock& rb : rblocks) {
         int li = 0, acc = nblocks[0];
@@ -649,15 +667,23 @@ struct Model::Impl {
         }
         if (bottleneck) {
           gemm1x1(kC1[li], rb.c1, x, Y1, nb * Fi * Ti, kActRelu, nullptr, s);
-          if (rb.stride == 1 && img_ok(rb.c2, rb.planes)) {
-            const Conv3x3Args a{Y1, Y2, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, nullptr, 1, conv3x3_img_on};
-            run(kK3[li], 2.0 * nb * Fi * Ti * rb.c2.N * rb.c2.K, s,
-                [&] { launch_conv3x3_img(a, rb.planes, s); });
+          if (rb.stride == 1 && res_tail && rb.w3acc && img_ok(rb.c2, rb.planes)) {
+            // conv2 + conv3 + residual in one launch, y2 in registers (bottleneck_tail)
+            const BottleneckTailArgs a{Y1, res, o, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.w3acc, rb.c3.bias};
+            const double pos = (double)nb * Fi * Ti;
+            run(kTl[li], 2.0 * pos * (rb.c2.N * rb.c2.K + rb.c3.N * rb.c3.K), s,
+                [&] { launch_bottleneck_tail(a, rb.planes, s); });
           } else {
-            gemm2d(kK3[li], rb.c2, Y1, rb.planes, Y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0,
-                   s);
+            if (rb.stride == 1 && img_ok(rb.c2, rb.planes)) {
+              const Conv3x3Args a{Y1, Y2, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, nullptr, 1,
+                                  conv3x3_img_on};
+              run(kK3[li], 2.0 * nb * Fi * Ti * rb.c2.N * rb.c2.K, s, [&] { launch_conv3x3_img(a, rb.planes, s); });
+            } else {
+              gemm2d(kK3[li], rb.c2, Y1, rb.planes, Y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0,
+                     s);
+            }
+            gemm1x1(kC3[li], rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
           }
-          gemm1x1(kC3[li], rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
         } else {
           if (rb.stride == 1 && img_ok(rb.c1, rb.planes)) {
             const Conv3x3Args a{x, Y1, nb, Fi, Ti, rb.c1.frag, rb.c1.bias, rb.c1.scale, rb.c1.shift, nullptr, 1, conv3x3_img_on};
@@ -1009,13 +1035,8 @@ struct Model::Impl {
     run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch(g, cw, s); });
   }
   void launch(const ConvGemmArgs& g, const ConvW& cw, hipStream_t s) {
-    // x3_variant 2 / 9: LDS-DMA staged kernels (conv_gemm_dma.hip variants 0 / 2) where
-    // their operand layouts allow, else the register-staged variant 5
-    const int dv = x3_variant == 2 ? 0 : x3_variant == 9 ? 2 : -1;
-    if (precision == 1 && dv >= 0 && conv_gemm_dma_v_supported(g, dv))
-      launch_conv_gemm_dma_v(g, cw.whi, cw.wlo, dv, s);
-    else if (precision == 1)
-      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_base(), s);
+    if (precision == 1)
+      launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant, s);
     else
       launch_conv_gemm(g, s);
   }
@@ -1083,7 +1104,7 @@ struct Model::Impl {
     double* sesum = reinterpret_cast<double*>(ws + off[16]);
     // SE squeeze fused into conv3's epilogue (per-utterance f64 column sums) on the
     // bf16x3 path for uniform batches whose utterances span >= one block of rows
-    const int se_bm = precision == 1 ? conv_gemm_x3_block_rows(ConvGemmArgs{.N = C}, x3_base()) : 0;
+    const int se_bm = precision == 1 ? conv_gemm_x3_block_rows(ConvGemmArgs{.N = C}, x3_variant) : 0;
     const bool se_fused = precision == 1 && !seg && T >= se_bm;
 
     gemm("layer1", layer1, feats, feat_dim, x[1], C, M, T, 1, 2, kActRelu, s);
@@ -1179,7 +1200,7 @@ struct Model::Impl {
     }
     if (precision == 1 && astp_fused_on) {
       // linear2 + softmax over frames + attentive mean / std in one pass (astp_fused.hip)
-      AstpArgs a{att, xp, 1536, B, T, 1536, seg, pool2_frag, pool2.bias, 1e-7f, pooled, astp_fused_on};
+      AstpArgs a{att, xp, 1536, B, T, 1536, seg, pool2_frag, pool2.bias, 1e-7f, pooled};
       run("astp", 2.0 * M * 1536 * 128, s, [&] { launch_astp_fused(a, s); });
     } else {
       gemm("pool_linear2", pool2, att, 128, logit, 1536, M, T, 1, 0, kActNone, s);

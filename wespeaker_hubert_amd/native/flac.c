@@ -198,8 +198,16 @@ static int read_utf8_number(Bits* b, uint64_t* v) {
 int wsp_flac_decode(const uint8_t* data, size_t n, int32_t** out, int* channels, int* sample_rate, int* bits,
                     int64_t* n_samples, char* err, int errlen) {
   *out = NULL;
-  if (n < 4 || memcmp(data, "fLaC", 4) != 0) FAIL("not a FLAC stream (no fLaC marker)");
-  size_t pos = 4;
+  size_t pos = 0;
+  /* a leading ID3v2 tag ("ID3", version, flags, syncsafe 28-bit size; a footer
+   * flag adds 10 bytes), as common decoders tolerate */
+  if (n >= 10 && memcmp(data, "ID3", 3) == 0) {
+    const size_t sz = ((size_t)(data[6] & 0x7F) << 21) | ((size_t)(data[7] & 0x7F) << 14) |
+                      ((size_t)(data[8] & 0x7F) << 7) | (size_t)(data[9] & 0x7F);
+    pos = 10 + sz + ((data[5] & 0x10) ? 10 : 0);
+  }
+  if (pos + 4 > n || memcmp(data + pos, "fLaC", 4) != 0) FAIL("not a FLAC stream (no fLaC marker)");
+  pos += 4;
   int have_info = 0, last = 0;
   int si_rate = 0, si_ch = 0, si_bps = 0, si_maxbs = 0;
   uint64_t si_total = 0;
@@ -239,6 +247,10 @@ int wsp_flac_decode(const uint8_t* data, size_t n, int32_t** out, int* channels,
   size_t done = 0;
   int rate = si_rate, bps = si_bps, rc = 0;
   while (pos < n) {
+    /* a trailing ID3v1 tag ("TAG" + 125 bytes), or padding after the last frame
+     * once STREAMINFO's sample count is decoded, ends the stream */
+    if (n - pos >= 3 && memcmp(data + pos, "TAG", 3) == 0) break;
+    if (si_total && done >= si_total) break;
     const size_t f0 = pos;
     Bits b = {data, n, pos * 8, 0};
     if (get_bits(&b, 14) != 0x3FFE) { snprintf(err, (size_t)errlen, "lost frame sync at byte %zu", pos); rc = -1; break; }

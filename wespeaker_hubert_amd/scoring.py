@@ -106,6 +106,32 @@ def compute_c_norm(fnr, fpr, p_target, c_miss=1, c_fa=1):
     return c_det / min(c_miss * p_target, c_fa * (1 - p_target))
 
 
+def plot_det_curve(fnr, fpr, save_path: str) -> None:
+    """score_metrics.py:119-160: the DET curve on normal-deviate axes with the EER
+    point marked, saved to `save_path` (matplotlib, non-interactive backend)."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    from scipy.stats import norm
+    ticks = [0.0001, 0.0002, 0.0005, 0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.4]
+    plt.plot(norm.ppf(fpr), norm.ppf(fnr), "r")
+    plt.xticks(norm.ppf(ticks), [str(x * 100) for x in ticks])
+    plt.yticks(norm.ppf(ticks), [str(x * 100) for x in ticks])
+    plt.xlim(norm.ppf([0.00051, 0.5]))
+    plt.ylim(norm.ppf([0.00051, 0.5]))
+    plt.xlabel("false-alarm rate [%]", fontsize=12)
+    plt.ylabel("false-reject rate [%]", fontsize=12)
+    eer = compute_eer(fnr, fpr)
+    plt.plot(norm.ppf(eer), norm.ppf(eer), "o")
+    plt.annotate("EER = %.2f%%" % (eer * 100), xy=(norm.ppf(eer), norm.ppf(eer)), xycoords="data",
+                 xytext=(norm.ppf(eer + 0.05), norm.ppf(eer + 0.05)), textcoords="data",
+                 arrowprops=dict(arrowstyle="-|>", connectionstyle="arc3, rad=+0.2", fc="w"), size=12,
+                 va="center", ha="center", bbox=dict(boxstyle="round4", fc="w"))
+    plt.grid()
+    plt.savefig(save_path)
+    plt.clf()
+
+
 # --------------------------------------------------------- file drivers ---
 def read_trials(path: str) -> List[List[str]]:
     with open(path, "r", encoding="utf8") as f:
