@@ -87,10 +87,10 @@ def test_residual_prefetch_bit_identical(arch, B, T):
 
 
 
-def _tail_pair(arch, seed, feat_dim):
+def _tail_pair(arch, seed, feat_dim, on=1):
     from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
     ms, sd = [], None
-    for on in (1, 0):
+    for on in (on, 0):
         m = HipSpeakerModel(arch, feat_dim=feat_dim, embed_dim=256)
         m.set_option("res_tail", on)
         if sd is None:
@@ -102,16 +102,18 @@ def _tail_pair(arch, seed, feat_dim):
 
 # feat_dim 40: stage 3 runs at F = 10, a partial 4-row frequency tile; T = 37 / 100 / 150
 # leave partial 32- / 64-frame time tiles
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("arch,B,T,F", [("ResNet50", 3, 100, 80), ("ResNet50", 2, 37, 40),
                                         ("ResNet101", 1, 150, 80), ("ResNet293", 2, 64, 80),
                                         ("ResNet152", 2, 45, 40)])
-def test_res_tail_matches_unfused_and_oracle(arch, B, T, F):
+def test_res_tail_matches_unfused_and_oracle(arch, B, T, F, mode):
     """Option res_tail (conv3x3_img.hip bottleneck_tail: conv2 + conv3 + residual in one
     launch, conv2's output kept in registers as conv3's A operand with a permuted k
-    order) against the two-launch path (conv3x3_img + conv_gemm_x3) and the oracle.
-    The same bf16x3 products are summed in a different k order inside conv3's MFMAs, so
-    the two agree to fp32 rounding, not bitwise."""
-    tail, plain, sd = _tail_pair(arch, 41, F)
+    order; mode 1 also runs the next block's conv1 on the output chunks staged in LDS)
+    against the unfused launches (conv3x3_img + conv_gemm_x3) and the oracle.  The same
+    bf16x3 products are summed in a different k order inside the MFMAs, so the paths
+    agree to fp32 rounding, not bitwise."""
+    tail, plain, sd = _tail_pair(arch, 41, F, mode)
     x = torch.from_numpy(synth_feats(19, B, T, F)).to(DEV)
     a = tail.embed(x).cpu().numpy()
     b = plain.embed(x).cpu().numpy()
@@ -122,8 +124,9 @@ def test_res_tail_matches_unfused_and_oracle(arch, B, T, F):
     assert np.abs(a - ref.numpy()).max() < 1e-4
 
 
-def test_res_tail_batch_rows_equal_batch_of_one():
-    tail, _, _ = _tail_pair("ResNet50", 42, 80)
+@pytest.mark.parametrize("mode", [1, 2])
+def test_res_tail_batch_rows_equal_batch_of_one(mode):
+    tail, _, _ = _tail_pair("ResNet50", 42, 80, mode)
     x = torch.from_numpy(synth_feats(20, 5, 123, 80)).to(DEV)
     full = tail.embed(x).cpu().numpy()
     for i in (0, 2, 4):

@@ -44,6 +44,11 @@ struct BottleneckTailArgs {
   const float* b2;
   const void* w3;
   const float* b3;
+  // optional: the NEXT block's conv1 (1x1, 4C -> C, bn1 folded, ReLU) on `out` while it is on
+  // chip: w1n = pack_frag B fragments [4C/16][hi, lo][C/32][64][8], y1n [B][F][T][C]
+  const void* w1n = nullptr;
+  const float* b1n = nullptr;
+  float* y1n = nullptr;
 };
 bool bottleneck_tail_supported(int C);
 void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s);

@@ -146,7 +146,8 @@ struct Model::Impl {
   int conv3x3_img_on = 2;
   int res_prefetch = 1;  // ResNet 1x1 residual convs: residual loaded ahead of the last k-tiles (option "res_prefetch")
   // ResNet bottleneck conv2 + conv3 (+ residual) of stride-1 blocks with planes 32 / 64 / 128 in one
-  // launch, y2 kept in registers (conv3x3_img.hip bottleneck_tail; option "res_tail")
+  // launch, y2 kept in registers (conv3x3_img.hip bottleneck_tail; option "res_tail"): 1 = also the
+  // next block's conv1 on the tail's output while it is on chip, 2 = the tail alone, 0 = off
   int res_tail = 1;
   bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
   int res2_variant = 0;  // res2_chain.hip kernel variant (option "res2_variant")
@@ -172,6 +173,7 @@ struct Model::Impl {
   struct RBlock {
     ConvW c1, c2, c3, sc;
     void* w3acc = nullptr;  // conv3 (bn3 folded) as pack_frag_acc B fragments for bottleneck_tail
+    void* w1frag = nullptr;  // conv1 (bn1 folded) as pack_frag B fragments: run inside the previous block's tail
     bool has_sc = false;
     int stride = 1, in_planes = 0, planes = 0, out_planes = 0;
   };
@@ -465,7 +467,7 @@ struct Model::Impl {
 
   // conv -> BN (eval) folded into the weights: W' = W * s[n], bias = shift.
   ConvW pack_conv_bn(const std::string& wname, const std::string& bn, int N, int cin, int taps,
-                     void** acc_frag = nullptr) {
+                     void** acc_frag = nullptr, void** b_frag = nullptr) {
     std::vector<double> sc, sh;
     bn_affine(bn, sc, sh);
     std::vector<float> w = P(wname);
@@ -475,6 +477,7 @@ struct Model::Impl {
     for (int n = 0; n < N; ++n) b[n] = (float)sh[n];
     ConvW cw = pack_conv(w, N, cin, taps, b.data(), "");
     if (acc_frag) *acc_frag = pack_frag_acc(w, N, cin * taps);
+    if (b_frag) *b_frag = pack_frag(w, N, cin * taps);
     if (taps == 9 && N == cin && conv3x3_img_supported(cin)) {
       // the same k = tap * cin + c order as the implicit GEMM's packed image
       std::vector<float> wk((size_t)N * 9 * cin);
@@ -505,7 +508,12 @@ struct Model::Impl {
         RBlock& rb = rblocks[idx_b++];
         const std::string p = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
         if (bottleneck) {
-          rb.c1 = pack_conv_bn(p + ".conv1.weight", p + ".bn1", rb.planes, rb.in_planes, 1);
+          // a stride-1 block whose input has 4 x its planes (every block after the first of a
+          // stage) runs its conv1 inside the previous block's bottleneck_tail
+          const bool c1_in_tail = rb.stride == 1 && rb.in_planes == 4 * rb.planes && bi > 0 &&
+                                  bottleneck_tail_supported(rb.planes);
+          rb.c1 = pack_conv_bn(p + ".conv1.weight", p + ".bn1", rb.planes, rb.in_planes, 1, nullptr,
+                               c1_in_tail ? &rb.w1frag : nullptr);
           rb.c2 = pack_conv_bn(p + ".conv2.weight", p + ".bn2", rb.planes, rb.planes, 9);
           rb.c3 = pack_conv_bn(p + ".conv3.weight", p + ".bn3", rb.out_planes, rb.planes, 1,
                                rb.stride == 1 && bottleneck_tail_supported(rb.planes) ? &rb.w3acc : nullptr);
@@ -655,6 +663,8 @@ struct Model::Impl {
       static const char* kK3[4] = {"res_conv3x3.L1", "res_conv3x3.L2", "res_conv3x3.L3", "res_conv3x3.L4"};
       static const char* kTl[4] = {"res_tail.L1", "res_tail.L2", "res_tail.L3", "res_tail.L4"};
       int ib = 0;
+      bool y1_ready = false;  // this block's conv1 output was written by the previous block's tail
+      float* y1_next = nullptr;
       for (const RBlock& rb : rblocks) {
         int li = 0, acc = nblocks[0];
         while (li < 3 && ib >= acc) acc += nblocks[++li];
@@ -666,13 +676,31 @@ struct Model::Impl {
           res = SC;
         }
         if (bottleneck) {
-          gemm1x1(kC1[li], rb.c1, x, Y1, nb * Fi * Ti, kActRelu, nullptr, s);
+          if (!y1_ready) gemm1x1(kC1[li], rb.c1, x, Y1, nb * Fi * Ti, kActRelu, nullptr, s);
+          const float* y1 = y1_ready ? y1_next : Y1;
+          y1_ready = false;
           if (rb.stride == 1 && res_tail && rb.w3acc && img_ok(rb.c2, rb.planes)) {
-            // conv2 + conv3 + residual in one launch, y2 in registers (bottleneck_tail)
-            const BottleneckTailArgs a{Y1, res, o, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.w3acc, rb.c3.bias};
+            // conv2 + conv3 + residual in one launch, y2 in registers (bottleneck_tail); with
+            // res_tail 1 also the next block's conv1 on this block's output (into the buffer
+            // the tail does not read)
+            const RBlock* nx = (size_t)ib < rblocks.size() ? &rblocks[ib] : nullptr;
+            // (the next block must run the tail too: its conv2 then reads y1 from either buffer)
+            const bool fuse1 = res_tail == 1 && nx && nx->w1frag && nx->planes == rb.planes && nx->w3acc &&
+                               nx->stride == 1 && img_ok(nx->c2, nx->planes);
+            BottleneckTailArgs a{y1, res, o, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.w3acc, rb.c3.bias};
+            float* y1n = y1 == Y1 ? Y2 : Y1;
+            if (fuse1) {
+              a.w1n = nx->w1frag;
+              a.b1n = nx->c1.bias;
+              a.y1n = y1n;
+            }
             const double pos = (double)nb * Fi * Ti;
-            run(kTl[li], 2.0 * pos * (rb.c2.N * rb.c2.K + rb.c3.N * rb.c3.K), s,
+            run(kTl[li], 2.0 * pos * (rb.c2.N * rb.c2.K + rb.c3.N * rb.c3.K + (fuse1 ? nx->c1.N * nx->c1.K : 0)), s,
                 [&] { launch_bottleneck_tail(a, rb.planes, s); });
+            if (fuse1) {
+              y1_ready = true;
+              y1_next = y1n;
+            }
           } else {
             if (rb.stride == 1 && img_ok(rb.c2, rb.planes)) {
               const Conv3x3Args a{Y1, Y2, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, nullptr, 1,
