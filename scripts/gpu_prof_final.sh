@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 R=${ROUND_TAG:-r2b}
 for c in ${CONFIGS:-c2}; do
   case $c in
-    c2) EXTRA="" ; BARGS="--steps 10 --warmup 2 --no-cpu-baseline" ;;
+    c2) EXTRA="--configs none" ; BARGS="--steps 10 --warmup 2 --no-cpu-baseline" ;;
     c3) EXTRA="--arch ResNet293" ; BARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-f32 --sustain-seconds 0" ;;
     c4) EXTRA="--arch HuBERT_ECAPA_GLOB_c512" ; BARGS="--steps 5 --warmup 1 --no-cpu-baseline --no-f32 --sustain-seconds 0" ;;
   esac
