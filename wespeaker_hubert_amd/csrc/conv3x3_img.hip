@@ -585,10 +585,14 @@ void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s) {
     launch_tail_k<32, 4, 32, 1, 3, 1>(p, s);  // 128 positions, 4 waves, 26 KB image: 3 blocks / CU
   else if (C == 32)
     launch_tail_k<32, 4, 64, 1, 4, 1>(p, s);  // 256 positions, 8 waves, 50 KB image: 2 blocks / CU
-  else if (C == 64)
+  else if (C == 64)  // (a 2 x 32 tile: C3 -1.3 %)
     launch_tail_k<64, 4, 32, 1, 3, 2, 1, 2>(p, s);  // 128 positions, 4 waves, 51 KB image: 3 blocks / CU
-  else  // (a 2 x 32 tile, two 70 KB blocks per CU, measured 1 % slower on C3)
-    launch_tail_k<128, 4, 32, 2, 2, 2, 1>(p, s);  // 128 positions, 8 waves (2 per position run), 102 KB image
+  else if (p.w1n)
+    // with the next conv1 (per-chunk barriers), two independent blocks per CU: C3 +1.5 % over the
+    // 4 x 32 tile (one 102 KB block per CU)
+    launch_tail_k<128, 2, 32, 2, 2, 2, 1>(p, s);  // 64 positions, 4 waves, 70 KB image: 2 blocks / CU
+  else
+    launch_tail_k<128, 4, 32, 2, 2, 2, 1>(p, s);  // 128 positions, 8 waves, 102 KB image  // 128 positions, 8 waves (2 per position run), 102 KB image
   WSP_HIP(hipGetLastError());
 }
 
