@@ -5,8 +5,8 @@
 // this file holds the rest:
 //
 //   conv0 + GroupNorm(512, 512) + GELU : waveform -> [B][T0][512]
-//       (1 input channel, k10 s5: 10 MACs per output — VALU, recomputed per
-//        pass instead of round-tripping 33 MB/utt of pre-norm activations)
+//       (1 input channel, k10 s5: 10 MACs per output — VALU; the GroupNorm
+//        statistics come from 65 f64 moments of the waveform, not from a pass over y)
 //   layernorm  : rows of D in {512, 768}, optional (remapped) residual add,
 //                optional s3prl Featurizer accumulation + length match
 //   cmn_rows   : per-utterance mean removal over frames (dataset_utils.py:19-26)
@@ -24,17 +24,69 @@ __device__ __forceinline__ float gelu_erf(float x) { return gelu_as(x); }
 // ---------------------------------------------------------------- conv0 ---
 constexpr int kC0 = 512, kK0 = 10, kS0 = 5, kTC = 128;
 
-// PASS 0: stats[0][b][c] += sum_t y, stats[1][b][c] += sum_t y^2 (f64);
-// PASS 2: out = GELU(GroupNorm(y)).  One thread per channel, one block per
-// (128-frame chunk, utterance); the waveform chunk is staged in LDS and read
-// as a broadcast.
+// GroupNorm(512, 512) normalises every channel over the utterance's frames.  Its
+// statistics need no pass over conv0's output: y_t[c] = sum_k w[c][k] x[5t + k], so
+//   sum_t y_t[c]   = sum_k w[c][k] S_k,            S_k  = sum_t x[5t + k]
+//   sum_t y_t[c]^2 = sum_jk w[c][j] w[c][k] R_jk,   R_jk = sum_t x[5t + j] x[5t + k]
+// — 10 + 55 moments of the (strided) waveform per utterance (conv0_moments_kernel,
+// f64), combined with each channel's weights where they are used (conv0_kernel).
+// The former statistics pass recomputed conv0 for all 512 channels of every frame
+// (0.8 ms of C4's 65 ms step); the moments read the waveform once.
+constexpr int kNM = kK0 + kK0 * (kK0 + 1) / 2;  // 65 moments per utterance
+constexpr int kMT = 1024;                        // frames per moments block
+
+__global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restrict__ wav, int N_, int ldw, int T0_,
+                                                            double* __restrict__ mom, const int* __restrict__ wseg,
+                                                            const int* __restrict__ oseg) {
+  __shared__ float xs[kMT * kS0 + kK0];
+  __shared__ double red[4][kNM];
+  const int b = blockIdx.y, t0 = blockIdx.x * kMT, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = wseg ? wseg[b + 1] - wseg[b] : N_;
+  const int T0 = oseg ? oseg[b + 1] - oseg[b] : T0_;
+  if (t0 >= T0) return;  // block-uniform: past this utterance
+  const float* x = wav + (wseg ? (size_t)wseg[b] : (size_t)b * ldw);
+  for (int i = tid; i < kMT * kS0 + kK0; i += 256) {
+    const int n = t0 * kS0 + i;
+    xs[i] = n < N ? x[n] : 0.f;
+  }
+  __syncthreads();
+  double m[kNM];
+#pragma unroll
+  for (int i = 0; i < kNM; ++i) m[i] = 0.0;
+  const int nt = min(kMT, T0 - t0);
+  for (int t = tid; t < nt; t += 256) {
+    double v[kK0];
+#pragma unroll
+    for (int k = 0; k < kK0; ++k) v[k] = (double)xs[t * kS0 + k];
+    int q = kK0;
+#pragma unroll
+    for (int j = 0; j < kK0; ++j) {
+      m[j] += v[j];
+#pragma unroll
+      for (int k = j; k < kK0; ++k, ++q) m[q] = fma(v[j], v[k], m[q]);
+    }
+  }
+  // fixed-order reduction: lanes (butterfly), waves (LDS), then one f64 atomic per
+  // moment and block (block order varies: the sums are exact to ~1e-16 relative)
+#pragma unroll
+  for (int i = 0; i < kNM; ++i) {
+    double v = m[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wave][i] = v;
+  }
+  __syncthreads();
+  if (tid < kNM) atomicAdd(&mom[(size_t)b * kNM + tid], red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]);
+}
+
+// out = GELU(GroupNorm(y)).  One thread per channel, one block per (128-frame chunk,
+// utterance); the waveform chunk is staged in LDS and read as a broadcast.
 // Segmented batch (wseg / oseg non-null): utterance b = samples [wseg[b], wseg[b+1])
 // -> output rows [oseg[b], oseg[b+1]); GroupNorm statistics per utterance as before.
-template <int PASS>
 __global__ __launch_bounds__(kC0) void conv0_kernel(const float* __restrict__ wav, int N_, int ldw, int T0_,
                                                     const float* __restrict__ w, const float* __restrict__ gamma,
-                                                    const float* __restrict__ beta, double* __restrict__ stats,
-                                                    float* __restrict__ out, int B, const int* __restrict__ wseg,
+                                                    const float* __restrict__ beta, const double* __restrict__ mom,
+                                                    float* __restrict__ out, const int* __restrict__ wseg,
                                                     const int* __restrict__ oseg) {
   __shared__ float xs[kTC * kS0 + kK0];
   const int b = blockIdx.y, t0 = blockIdx.x * kTC, c = threadIdx.x;
@@ -50,35 +102,33 @@ __global__ __launch_bounds__(kC0) void conv0_kernel(const float* __restrict__ wa
   float wr[kK0];
 #pragma unroll
   for (int k = 0; k < kK0; ++k) wr[k] = w[c * kK0 + k];
-  __syncthreads();
-  const int nt = min(kTC, T0 - t0);
-  double* s0 = stats + (size_t)b * kC0 + c;
-  double* s1 = stats + (size_t)(B + b) * kC0 + c;
-  // PASS 0: first and second moments in f64 (one conv pass: var = E[y^2] - mean^2,
-  // exact enough in f64 for fp32 outputs); PASS 2: normalise + affine + GELU + store.
-  float scale = 1.f, shift = 0.f;
-  if (PASS == 2) {
-    const double m = *s0 / T0;
-    const double var = fmax(*s1 / T0 - m * m, 0.0);
+  // this channel's first and second moments from the utterance's waveform moments (f64;
+  // var = E[y^2] - mean^2 is exact enough in f64 for fp32 outputs)
+  float scale, shift;
+  {
+    const double* mo = mom + (size_t)b * kNM;
+    double s0 = 0.0, s1 = 0.0;
+    int q = kK0;
+#pragma unroll
+    for (int j = 0; j < kK0; ++j) {
+      const double wj = (double)wr[j];
+      s0 = fma(wj, mo[j], s0);
+#pragma unroll
+      for (int k = j; k < kK0; ++k) s1 = fma((k == j ? 1.0 : 2.0) * wj * (double)wr[k], mo[q++], s1);
+    }
+    const double mean = s0 / T0;
+    const double var = fmax(s1 / T0 - mean * mean, 0.0);
     const float rstd = (float)(1.0 / sqrt(var + 1e-5));
     scale = rstd * gamma[c];
-    shift = beta[c] - (float)m * scale;
+    shift = beta[c] - (float)mean * scale;
   }
-  double acc = 0.0, acc2 = 0.0;
+  __syncthreads();
+  const int nt = min(kTC, T0 - t0);
   for (int t = 0; t < nt; ++t) {
     float y = 0.f;
 #pragma unroll
     for (int k = 0; k < kK0; ++k) y = fmaf(wr[k], xs[t * kS0 + k], y);
-    if (PASS == 0) {
-      acc += (double)y;
-      acc2 = fma((double)y, (double)y, acc2);
-    } else {
-      out[(obase + t0 + t) * kC0 + c] = gelu_erf(fmaf(y, scale, shift));
-    }
-  }
-  if (PASS == 0) {
-    atomicAdd(s0, acc);
-    atomicAdd(s1, acc2);
+    out[(obase + t0 + t) * kC0 + c] = gelu_erf(fmaf(y, scale, shift));
   }
 }
 
@@ -198,12 +248,11 @@ void launch_hubert_conv0(const float* wav, int B, int N, int ldw, int T0, const 
     WSP_CHECK(ldw >= N, "hubert conv0: ldw < N");
   }
   WSP_CHECK(B > 0 && T0 > 0, "hubert conv0: empty batch");  // segmented: T0 = longest utterance's frames
-  WSP_HIP(hipMemsetAsync(stats, 0, sizeof(double) * 2 * B * kC0, s));
-  const dim3 grid((T0 + kTC - 1) / kTC, B);
-  hipLaunchKernelGGL(conv0_kernel<0>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B, wseg,
-                     oseg);
-  hipLaunchKernelGGL(conv0_kernel<2>, grid, dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta, stats, out, B, wseg,
-                     oseg);
+  WSP_HIP(hipMemsetAsync(stats, 0, sizeof(double) * kNM * B, s));  // kNM <= 2 * kC0 doubles per utterance
+  hipLaunchKernelGGL(conv0_moments_kernel, dim3((T0 + kMT - 1) / kMT, B), dim3(256), 0, s, wav, N, ldw, T0, stats,
+                     wseg, oseg);
+  hipLaunchKernelGGL(conv0_kernel, dim3((T0 + kTC - 1) / kTC, B), dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta,
+                     stats, out, wseg, oseg);
   WSP_HIP(hipGetLastError());
 }
 

@@ -157,7 +157,7 @@ void launch_fbank(const void* wav, int dtype, int B, int N, int ld, float scale,
 
 // HuBERT-base front end (hubert.hip).
 // conv0 (1 -> 512, k10 s5, no bias) + GroupNorm(512, 512) + GELU:
-// wav [B][ldw] (N samples) -> out [B][T0][512]; stats = [2][B][512] doubles scratch.
+// wav [B][ldw] (N samples) -> out [B][T0][512]; stats = [2][B][512] doubles scratch (65 per utterance used).
 // Segmented: wseg / oseg = device int32 [B+1] sample / output-row offsets, T0 = frames of
 // the longest utterance.
 void launch_hubert_conv0(const float* wav, int B, int N, int ldw, int T0, const float* w, const float* gamma,
