@@ -164,12 +164,15 @@ def test_ragged_batch_equals_batch_of_one(sd_np, sd_t, layer, multi):
 
 
 @pytest.mark.parametrize("W", [16000, 100000])
-def test_lds_attention_matches_oracle(sd_np, sd_t, W):
-    """attn.hip (K / V staged once per 256-key block in LDS) against the oracle;
-    W = 100000 gives 312 frames: two query blocks and two key blocks per
-    (utterance, head)."""
+@pytest.mark.parametrize("pipe", [1, 0])
+def test_lds_attention_matches_oracle(sd_np, sd_t, W, pipe):
+    """attn.hip — the persistent pipelined kernel (keys in LDS halves of 128, the next
+    half in flight) and the one-block-per-(utterance, head) kernel — against the oracle;
+    W = 100000 gives 312 frames: two query blocks and three key halves per (utterance,
+    head)."""
     wav = _wav(17, 2, W)
     fe = _frontend(sd_np)
+    fe.set_option("attn_pipe", pipe)
     got = fe.extract(torch.from_numpy(wav).to(DEV)).cpu()
     with torch.no_grad():
         ref = hubert_ref.s3prl_frontend(torch.from_numpy(wav), sd_t)

@@ -319,7 +319,7 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
     const HLayer& L = h_layers[l];
     conv("h_qkv", L.qkv, x, kHidden, qkv, 3 * kHidden, M, M, 1, 0, kActNone, nullptr, true, nullptr, nullptr, 0);
     run("h_attn", 4.0 * B * kHeads * (double)pl.maxT6 * pl.maxT6 * (kHidden / kHeads), s,
-        [&] { launch_attn(qkv, 3 * kHidden, ao, kHidden, B, pl.maxT6, kHeads, kHidden / kHeads, s, seg6); });
+        [&] { launch_attn(qkv, 3 * kHidden, ao, kHidden, B, pl.maxT6, kHeads, kHidden / kHeads, s, seg6, attn_pipe); });
     conv("h_out_proj", L.out, ao, kHidden, x1, kHidden, M, M, 1, 0, kActNone, x, true, nullptr, nullptr, 0);
     ln("h_ln", x1, nullptr, x, M, kHidden, L.ln1_g, L.ln1_b, -1);
     conv("h_fc1", L.fc1, x, kHidden, ffn, kFfn, M, M, 1, 0, kActGelu, nullptr, true, nullptr, nullptr, 0);
