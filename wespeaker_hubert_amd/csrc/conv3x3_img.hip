@@ -233,6 +233,9 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
   constexpr int CH = WN * NC * 32, KK = CH / 16, CBR = 2 * CH, NPR = G::NW / WN;
   constexpr int NT1 = C / 32, TN1 = NT1 / WN;  // next conv1: output tiles, per wave
   static_assert(!FUSE1 || (KK % 2 == 0 && 2 * NPR * 32 * CBR <= G::LDS), "conv1 chunk buffer");
+  // two chunk buffers where the image's LDS holds them: one barrier per chunk instead of two
+  constexpr int CBUF = 2 * NPR * 32 * CBR;
+  constexpr bool CB2 = 2 * CBUF <= G::LDS;
   static_assert(WN == 1 || G::IR * G::RB * 2 >= G::NW / WN * KS3 * 2048, "y2 exchange must fit the image");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* xhi = smem;
@@ -379,8 +382,6 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
   }
   auto cbsw = [](int r) { return CBR == 64 ? ((r >> 2) & 3) : CBR == 128 ? ((r >> 1) & 7) : (r & 15); };
   auto cbaddr = [&](int prow, int c16) { return prow * CBR + ((c16 ^ cbsw(prow)) << 4); };
-  unsigned char* cbhi = smem;
-  unsigned char* cblo = smem + NPR * 32 * CBR;
   const __amdgpu_buffer_rsrc_t rw1 = make_rsrc(FUSE1 ? p.w1n : p.w3);
   // k-step kk of chunk `chunk`'s K block -> global k-step of W1 (4C-deep): the block holds
   // partner 0's NC tiles, then partner 1's
@@ -401,6 +402,8 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
 #pragma unroll 1
   for (int chunk = 0; chunk < NCH; ++chunk) {
     const int cb = (wn * NTW + chunk * NC) * 32 + r32;  // column of tile 0
+    unsigned char* cbhi = smem + (CB2 ? (chunk & 1) * CBUF : 0);
+    unsigned char* cblo = cbhi + NPR * 32 * CBR;
     bf16x8 u0h[FUSE1 ? TN1 : 1], u0l[FUSE1 ? TN1 : 1], u1h[FUSE1 ? TN1 : 1], u1l[FUSE1 ? TN1 : 1];
     if constexpr (FUSE1) {  // the chunk's first two W1 k-steps land during its conv3
       w1load(chunk, 0, u0h, u0l);
@@ -502,7 +505,7 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
         }
         if (kk + 3 < KK) w1load(chunk, kk + 3, u1h, u1l);
       }
-      __syncthreads();  // the chunk buffer is rewritten by the next chunk
+      if constexpr (!CB2) __syncthreads();  // the chunk buffer is rewritten by the next chunk
     }
   }
   if constexpr (FUSE1) {
