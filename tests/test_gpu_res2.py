@@ -19,13 +19,14 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-def _pair(arch, seed):
+def _pair(arch, seed, variant=0):
     from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
     ms = []
     sd = None
     for fused in (1, 0):
         m = HipSpeakerModel(arch, feat_dim=80, embed_dim=192)
         m.set_option("res2_fused", fused)
+        m.set_option("res2_variant", variant)
         if sd is None:
             sd = synth_state_dict(seed, m.state_dict_layout())
         m.load_state_dict(sd)
@@ -36,8 +37,10 @@ def _pair(arch, seed):
 @pytest.mark.parametrize("arch,B,T", [("ECAPA_TDNN_c1024", 3, 498), ("ECAPA_TDNN_c1024", 40, 498),
                                       ("ECAPA_TDNN_c512", 5, 263), ("ECAPA_TDNN_GLOB_c512", 3, 77),
                                       ("ECAPA_TDNN_GLOB_c1024", 2, 2), ("ECAPA_TDNN_c512", 7, 31)])
-def test_res2_fused_equals_chain_and_oracle(arch, B, T):
-    fused, chain, sd = _pair(arch, 11)
+@pytest.mark.parametrize("variant", [0, 3])
+def test_res2_fused_equals_chain_and_oracle(arch, B, T, variant):
+    """res2_variant 0: 128-row windows, 4 waves of 64 x 64; 3: 8 waves of 64 rows x 32 channels."""
+    fused, chain, sd = _pair(arch, 11, variant)
     x = torch.from_numpy(synth_feats(5, B, T, 80)).to(DEV)
     a = fused.embed(x).cpu().numpy()
     b = chain.embed(x).cpu().numpy()
@@ -49,8 +52,9 @@ def test_res2_fused_equals_chain_and_oracle(arch, B, T):
     assert np.abs(a[rows] - ref.numpy()).max() < 1e-4
 
 
-def test_res2_fused_ragged_equals_chain():
-    fused, chain, _ = _pair("ECAPA_TDNN_c1024", 12)
+@pytest.mark.parametrize("variant", [0, 3])
+def test_res2_fused_ragged_equals_chain(variant):
+    fused, chain, _ = _pair("ECAPA_TDNN_c1024", 12, variant)
     frames = [3, 77, 498, 150, 2, 263, 41, 300, 9]
     feats = np.concatenate([synth_feats(400 + i, 1, t, 80)[0] for i, t in enumerate(frames)])
     cat = torch.from_numpy(feats).to(DEV)

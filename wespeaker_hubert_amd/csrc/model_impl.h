@@ -150,7 +150,7 @@ struct Model::Impl {
   // next block's conv1 on the tail's output while it is on chip, 2 = the tail alone, 0 = off
   int res_tail = 1;
   bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
-  int res2_variant = 0;  // res2_chain.hip kernel variant (option "res2_variant")
+  int res2_variant = 3;  // res2_chain.hip kernel variant (option "res2_variant"; 3 = 8 waves, measured fastest)
   ConvW conv, pool1, pool2;
   // conv_cat on [out2, out3, g4 * h3_4]: out4 = out3 + g4 * h3_4, so W . [out2; out3; out4]
   // = W_a out2 + (W_b + W_c) out3 + W_c (g4 * h3_4) — the last SE block's residual pass

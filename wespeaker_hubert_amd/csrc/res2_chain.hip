@@ -42,7 +42,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kPad = 4;  // image rows beyond each window edge (max dilation)
 
-template <int W, int R, int WNv>
+template <int W, int R, int WNv, int NWv = R / 32>
 struct Geo {
   static constexpr int IR = R + 2 * kPad;          // image rows; row IR is the zero row
   static constexpr int RB = 2 * W;                 // bytes per image row and plane
@@ -50,7 +50,7 @@ struct Geo {
   static constexpr int KS = 3 * W / 16;            // 16-deep MFMA k-steps per conv (K = 3W)
   static constexpr int KC = W / 16;                // k-steps per tap
   static constexpr int WST = 64 * W;               // one k-step of W: W cols x 16 k x (hi, lo) bf16
-  static constexpr int NW = R / 32;                // waves: 4 (R = 128) or 8 (R = 256)
+  static constexpr int NW = NWv;                   // waves: R / 32 (4 for R = 128, 8 for 256), or 8 at R = 128
   static constexpr int WN = WNv, WM = NW / WN, TM = R / 32 / WM, TN = W / 32 / WN;
   static_assert(TN >= 1 && TM >= 1, "res2 wave layout");
   static constexpr int NT = NW * 64;
@@ -65,11 +65,10 @@ struct Geo {
 
 __device__ __forceinline__ unsigned short bf_bits(__bf16 x) { return __builtin_bit_cast(unsigned short, x); }
 
-template <int W, int R, int WNv>
-__global__ __launch_bounds__(2 * R, R == 128 ? 2 : 1) void res2_chain_kernel(const Res2Args p) {
-  using G = Geo<W, R, WNv>;
+template <int W, int R, int WNv, int NWv>
+__global__ __launch_bounds__(NWv * 64, R == 128 ? NWv / 2 : 1) void res2_chain_kernel(const Res2Args p) {
+  using G = Geo<W, R, WNv, NWv>;
   constexpr int TM = G::TM, TN = G::TN, NT = G::NT, IR = G::IR;
-  static_assert(NT == 2 * R, "launch bounds assume 2R threads");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* xhi = smem;
   unsigned char* xlo = smem + G::PLANE;
@@ -281,17 +280,20 @@ __global__ __launch_bounds__(2 * R, R == 128 ? 2 : 1) void res2_chain_kernel(con
 
 bool res2_chain_supported(int w, int dil) { return (w == 64 || w == 128) && dil >= 1 && dil <= kPad; }
 
-static int res2_rows(int variant) { return (variant & 1) ? 256 : 128; }
+static int res2_rows(int variant) { return variant == 1 ? 256 : 128; }
 
-template <int W, int R, int WN>
+template <int W, int R, int WN, int NW = R / 32>
 void launch_res2_k(const Res2Args& p, int nblk, hipStream_t s) {
-  hipLaunchKernelGGL((res2_chain_kernel<W, R, WN>), dim3(nblk), dim3(Geo<W, R, WN>::NT),
-                     (Geo<W, R, WN>::LDS), s, p);
+  hipLaunchKernelGGL((res2_chain_kernel<W, R, WN, NW>), dim3(nblk), dim3(Geo<W, R, WN, NW>::NT),
+                     (Geo<W, R, WN, NW>::LDS), s, p);
 }
 
 template <int W>
 void launch_res2_w(const Res2Args& p, int nblk, hipStream_t s) {
-  if (p.variant & 1) {
+  if (p.variant == 3) {
+    if constexpr (W == 128) launch_res2_k<W, 128, 4, 8>(p, nblk, s);  // 8 waves of 64 rows x 32 channels
+    else launch_res2_k<W, 128, 2, 8>(p, nblk, s);
+  } else if (p.variant & 1) {
     launch_res2_k<W, 256, 2>(p, nblk, s);
   } else if (p.variant & 2) {
     if constexpr (W == 128) launch_res2_k<W, 128, 4>(p, nblk, s);  // 1 x 4 waves: 128 rows x 32 channels
