@@ -431,6 +431,8 @@ def kernel_table(w, steps: int) -> dict:
     stream, wsp_model_profile), time per step and the class's algorithmic rate."""
     kernels = {}
     queries = [(w["model"], t) for t in HEAD_TAGS] + ([(w["fe"], t) for t in HUBERT_TAGS] if w["fe"] else [])
+    if w["fe"]:
+        queries += [(w["fe"], f"h_cnn.c{i}") for i in range(1, 7)]  # per-layer sub-classes of h_cnn
     for mm, tag in queries:
         n, ms, fl = mm.profile_query(tag)
         if n:

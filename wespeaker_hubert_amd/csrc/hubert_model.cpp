@@ -302,8 +302,10 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
     });
     float* src = cnnA;
     float* dst = cnnB;
+    // profiling sub-classes per layer: h_cnn.c<i>
+    static const char* kCnn[7] = {"", "h_cnn.c1", "h_cnn.c2", "h_cnn.c3", "h_cnn.c4", "h_cnn.c5", "h_cnn.c6"};
     for (int i = 1; i < 7; ++i) {
-      conv("h_cnn", h_conv[i], src, kConvDim, dst, kConvDim, (int)c.rows[i], (int)c.rows[i - 1], kConvS[i], 0,
+      conv(kCnn[i], h_conv[i], src, kConvDim, dst, kConvDim, (int)c.rows[i], (int)c.rows[i - 1], kConvS[i], 0,
            kActGelu, nullptr, false, lvl(i), lvl(i - 1), nb);
       std::swap(src, dst);
     }
