@@ -7,7 +7,7 @@
 // The 7 convs form a serial chain whose every step reads the previous step's
 // output: run as 7 GEMM launches, each step round-trips HBM (read sp + spx[i],
 // write sp).  Here a block owns `rout` output rows and keeps the chain on chip:
-//   * a window of kR = 256 frame rows (the owned rows plus a 6d halo on each
+//   * a window of R = 128 frame rows (the owned rows plus a 6d halo on each
 //     side) is the GEMM's M; step i is valid on window rows [i*d, kR - i*d)
 //     (the conv's +-d taps lose d rows per side per step), so after 7 steps the
 //     owned rows [6d, kR - 6d) are exact — halo recomputation instead of a
@@ -24,9 +24,14 @@
 //     fragments straight from global memory (1 KB contiguous per instruction,
 //     L1/L2-resident, two k-steps ahead in registers): the X image is the only
 //     LDS operand, constant during a step, and the k-loop has no barrier;
-//   * R = 128-row windows (4 waves, 70 KB of LDS) run two blocks per CU, so one
-//     block's epilogue (addend loads, stores, image update) overlaps the other's
-//     MFMA loop; R = 256 (8 waves, 136 KB) halves the halo overhead instead.
+//   * 128-row windows (70 KB of LDS) run two blocks per CU, so one block's
+//     epilogue (addend loads, stores, image update) overlaps the other's MFMA
+//     loop.  Default: 8 waves of 64 rows x 32 channels (res2_variant 3; C2
+//     1.63 -> 1.45 ms/step over 4 waves of 64 x 64).  Measured and dropped (r3):
+//     256-row windows (half the halo rows, one block per CU: 1.57 ms/step even
+//     with 4 W k-steps in flight).  Ablations of variant 3 (ms per launch, 0.486):
+//     no W reloads 0.416, no addend loads 0.422, no sp stores 0.446 — no single
+//     term dominates; the rest is the per-step barriers and image rewrite.
 // HBM traffic per row: spx[0..6] read once (+ halo re-reads, mostly L2 hits of
 // the neighbouring block) and sp_0..6 written once.
 #include "gemm_common.h"
@@ -65,7 +70,7 @@ struct Geo {
 
 __device__ __forceinline__ unsigned short bf_bits(__bf16 x) { return __builtin_bit_cast(unsigned short, x); }
 
-template <int W, int R, int WNv, int NWv>
+template <int W, int R, int WNv, int NWv, int PD>
 __global__ __launch_bounds__(NWv * 64, R == 128 ? NWv / 2 : 1) void res2_chain_kernel(const Res2Args p) {
   using G = Geo<W, R, WNv, NWv>;
   constexpr int TM = G::TM, TN = G::TN, NT = G::NT, IR = G::IR;
@@ -152,9 +157,11 @@ __global__ __launch_bounds__(NWv * 64, R == 128 ? NWv / 2 : 1) void res2_chain_k
       bl[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? o + (W / 32) * 1024 : kOOB, 0, 0));
     }
   };
-  bf16x8 wb0h[TN], wb0l[TN], wb1h[TN], wb1l[TN];
-  wload(0, wb0h, wb0l);
-  wload(1, wb1h, wb1l);
+  // W fragments of k-step k in ring slot k % PD (PD k-steps in flight)
+  static_assert(PD % 2 == 0 && G::KS % PD == 0, "res2 W prefetch depth");
+  bf16x8 wbh[PD][TN], wbl[PD][TN];
+#pragma unroll
+  for (int d = 0; d < PD; ++d) wload(d, wbh[d], wbl[d]);
   __syncthreads();
 
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(p.out);
@@ -172,7 +179,7 @@ __global__ __launch_bounds__(NWv * 64, R == 128 ? NWv / 2 : 1) void res2_chain_k
     }
   };
   // one 16-deep k-step g on the fragments in (ah, al) and (bh, bl); the W
-  // fragments are then reloaded with k-step g + 2
+  // fragments are then reloaded with k-step g + PD
   auto mma = [&](int g, const bf16x8 (&ah)[TM], const bf16x8 (&al)[TM], bf16x8 (&bh)[TN], bf16x8 (&bl)[TN]) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -182,9 +189,9 @@ __global__ __launch_bounds__(NWv * 64, R == 128 ? NWv / 2 : 1) void res2_chain_k
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
       }
-    wload(g + 2, bh, bl);
+    wload(g + PD, bh, bl);
   };
-  bf16x8 a0h[TM], a0l[TM], a1h[TM], a1l[TM];
+  bf16x8 ah2[2][TM], al2[2][TM];
 
 #pragma unroll 1
   for (int step = 0; step < 7; ++step) {
@@ -195,19 +202,20 @@ __global__ __launch_bounds__(NWv * 64, R == 128 ? NWv / 2 : 1) void res2_chain_k
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    // KS is even: k-steps in pairs, A and W fragments alternating between two
-    // register sets — k-step t+1's A fragments are read from LDS while k-step t's
-    // MFMAs run (the image only changes between steps)
-    read_a(0, a0h, a0l);
+    // k-steps in groups of PD: A fragments alternate between two register sets —
+    // k-step t+1's are read from LDS while k-step t's MFMAs run (the image only
+    // changes between steps) — and W comes from the ring
+    read_a(0, ah2[0], al2[0]);
 #pragma unroll 1
-    for (int t = 0; t < G::KS - 2; t += 2) {
-      read_a(t + 1, a1h, a1l);
-      mma(gb + t, a0h, a0l, wb0h, wb0l);
-      read_a(t + 2, a0h, a0l);
-      mma(gb + t + 1, a1h, a1l, wb1h, wb1l);
+    for (int t = 0; t < G::KS - PD; t += PD) {
+#pragma unroll
+      for (int u = 0; u < PD; ++u) {
+        read_a(t + u + 1, ah2[(u + 1) & 1], al2[(u + 1) & 1]);
+        mma(gb + t + u, ah2[u & 1], al2[u & 1], wbh[u], wbl[u]);
+      }
     }
     // the next conv's addend spx[step + 1] (accumulator layout: row per register,
-    // col = lane & 31), issued two k-steps before the epilogue.  Row offsets are
+    // col = lane & 31), issued PD k-steps before the epilogue.  Row offsets are
     // laundered per step (asm) so hipcc rebuilds them here instead of hoisting 64
     // per-element addresses out of the step loop into registers.
     int ldx4 = p.ldx * 4, ldo4 = p.ldo * 4, mw = wr0 + wm * TM * 32 + 4 * h;
@@ -231,9 +239,11 @@ __global__ __launch_bounds__(NWv * 64, R == 128 ? NWv / 2 : 1) void res2_chain_k
         }
       }
     }
-    read_a(G::KS - 1, a1h, a1l);
-    mma(gb + G::KS - 2, a0h, a0l, wb0h, wb0l);
-    mma(gb + G::KS - 1, a1h, a1l, wb1h, wb1l);
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      if (u + 1 < PD) read_a(G::KS - PD + u + 1, ah2[(u + 1) & 1], al2[(u + 1) & 1]);
+      mma(gb + G::KS - PD + u, ah2[u & 1], al2[u & 1], wbh[u], wbl[u]);
+    }
     __syncthreads();  // every wave is done reading X_step
 
     // ---- epilogue: sp = BN(ReLU(acc + b)); owned rows -> out; X_{step+1} -> LDS
@@ -280,11 +290,11 @@ __global__ __launch_bounds__(NWv * 64, R == 128 ? NWv / 2 : 1) void res2_chain_k
 
 bool res2_chain_supported(int w, int dil) { return (w == 64 || w == 128) && dil >= 1 && dil <= kPad; }
 
-static int res2_rows(int variant) { return variant == 1 ? 256 : 128; }
+static int res2_rows(int) { return 128; }
 
-template <int W, int R, int WN, int NW = R / 32>
+template <int W, int R, int WN, int NW = R / 32, int PD = 2>
 void launch_res2_k(const Res2Args& p, int nblk, hipStream_t s) {
-  hipLaunchKernelGGL((res2_chain_kernel<W, R, WN, NW>), dim3(nblk), dim3(Geo<W, R, WN, NW>::NT),
+  hipLaunchKernelGGL((res2_chain_kernel<W, R, WN, NW, PD>), dim3(nblk), dim3(Geo<W, R, WN, NW>::NT),
                      (Geo<W, R, WN, NW>::LDS), s, p);
 }
 
@@ -293,10 +303,8 @@ void launch_res2_w(const Res2Args& p, int nblk, hipStream_t s) {
   if (p.variant == 3) {
     if constexpr (W == 128) launch_res2_k<W, 128, 4, 8>(p, nblk, s);  // 8 waves of 64 rows x 32 channels
     else launch_res2_k<W, 128, 2, 8>(p, nblk, s);
-  } else if (p.variant & 1) {
-    launch_res2_k<W, 256, 2>(p, nblk, s);
-  } else if (p.variant & 2) {
-    if constexpr (W == 128) launch_res2_k<W, 128, 4>(p, nblk, s);  // 1 x 4 waves: 128 rows x 32 channels
+  } else if (p.variant == 2) {
+    if constexpr (W == 128) launch_res2_k<W, 128, 4, 4, 4>(p, nblk, s);  // 1 x 4 waves: 128 rows x 32 channels, 4 W k-steps in flight
     else launch_res2_k<W, 128, 2>(p, nblk, s);
   } else {
     launch_res2_k<W, 128, 2>(p, nblk, s);
