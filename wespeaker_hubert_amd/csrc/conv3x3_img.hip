@@ -221,7 +221,7 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void conv3x3_img_kernel(cons
 // its k-loop), then b3 + residual, ReLU, store.  y2 never exists in memory: per
 // position the HBM traffic is y1 (halo re-reads mostly L2 hits) + res + out instead
 // of conv2's y1 + y2 and conv3's y2 + res + out.
-template <int C, int FB, int TB, int WN, int MINB, int NC, bool FUSE1>
+template <int C, int FB, int TB, int WN, int MINB, int NC, bool FUSE1, int P1, int PM>
 __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(const BottleneckTailArgs p) {
   using G = Img<C, FB, TB, WN>;
   constexpr int TN = G::TN, PT = G::PT;
@@ -255,56 +255,81 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
   const size_t plane = (size_t)p.F * p.T;
   stage_patch<G>(make_rsrc(p.y1 + (size_t)b * plane * C), p.F, p.T, f0, t0, tid, xhi, xlo);
 
-  const int pr = wave / WN, wn = wave - pr * WN;  // position run, channel / column half
+  const int pr = wave / WN, wn = wave - pr * WN;  // phase-2 position run, column half
   const int lf = pr / (TB / 32);
   const int lt0 = (pr % (TB / 32)) * 32;
-  const int row0 = lf * PT + lt0 + r32;
 
-  // ---- phase 1: conv2 (this wave's TN channel tiles), transposed accumulators
+  // ---- phase 1: conv2, transposed accumulators.  PM = 1: the wave's own position run
+  // and its phase-2 channel half (TN tiles).  PM = 2: two position runs x TNP channel
+  // tiles per wave, so each W2 fragment fetched feeds two MFMA triples (half the vector
+  // memory instructions per MFMA; the y2 tiles are then regrouped through LDS).
+  constexpr int NR = FB * TB / 32;                              // position runs
+  constexpr int TNP = PM == 1 ? TN : G::CT * NR / (PM * G::NW);  // phase-1 channel tiles per wave
+  constexpr int NCG = G::CT / TNP;                              // phase-1 channel groups
+  static_assert(PM == 1 || (PM == 2 && NR % 2 == 0 && TNP >= 1 && (NR / PM) * NCG == G::NW),
+                "bottleneck_tail: phase-1 wave layout");
+  const int pg = wave / NCG, cg = wave - pg * NCG;  // PM = 1: pg = pr, cg = wn
+  int prow[PM];
+#pragma unroll
+  for (int i = 0; i < PM; ++i) {
+    const int run = pg * PM + i;
+    prow[i] = (run / (TB / 32)) * PT + (run % (TB / 32)) * 32 + r32;
+  }
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w2);
-  auto wload = [&](int g, bf16x8 (&bh)[TN], bf16x8 (&bl)[TN]) {
+  auto wload = [&](int g, bf16x8 (&bh)[TNP], bf16x8 (&bl)[TNP]) {
     const bool ok = g < G::KS;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int o = ((g * 2 * G::CT + wn * TN + j) * 64 + lane) * 16;
+    for (int j = 0; j < TNP; ++j) {
+      const int o = ((g * 2 * G::CT + cg * TNP + j) * 64 + lane) * 16;
       bh[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? o : kOOB, 0, 0));
       bl[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? o + G::CT * 1024 : kOOB, 0, 0));
     }
   };
-  auto read_b = [&](int g, bf16x8& xh, bf16x8& xl) {
+  auto read_b = [&](int g, bf16x8 (&xh)[PM], bf16x8 (&xl)[PM]) {
     const int tap = g / G::KC, cb = g - tap * G::KC;
     const int kf = tap / 3, kt = tap - kf * 3;
-    const int a = G::addr(row0 + kf * PT + kt, 2 * cb + h);
-    xh = *reinterpret_cast<const bf16x8*>(xhi + a);
-    xl = *reinterpret_cast<const bf16x8*>(xlo + a);
-  };
-  f32x16 acc[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-  auto mma_t = [&](const bf16x8& xh, const bf16x8& xl, const bf16x8 (&bh)[TN], const bf16x8 (&bl)[TN]) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], xl, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl[j], xh, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], xh, acc[j], 0, 0, 0);
+    for (int i = 0; i < PM; ++i) {
+      const int a = G::addr(prow[i] + kf * PT + kt, 2 * cb + h);
+      xh[i] = *reinterpret_cast<const bf16x8*>(xhi + a);
+      xl[i] = *reinterpret_cast<const bf16x8*>(xlo + a);
     }
   };
+  f32x16 acc[PM][TNP];
+#pragma unroll
+  for (int i = 0; i < PM; ++i)
+#pragma unroll
+    for (int j = 0; j < TNP; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto mma_t = [&](const bf16x8 (&xh)[PM], const bf16x8 (&xl)[PM], const bf16x8 (&bh)[TNP],
+                   const bf16x8 (&bl)[TNP]) {
+#pragma unroll
+    for (int i = 0; i < PM; ++i)
+#pragma unroll
+      for (int j = 0; j < TNP; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], xl[i], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl[j], xh[i], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], xh[i], acc[i][j], 0, 0, 0);
+      }
+  };
   {
-    bf16x8 b0h[TN], b0l[TN], b1h[TN], b1l[TN], x0h, x0l, x1h, x1l;
-    wload(0, b0h, b0l);
-    wload(1, b1h, b1l);
+    // W2 fragments of k-step g in ring slot g % P1 (P1 k-steps in flight: phase 1's live
+    // registers are few, so the ring can be deeper than the phase 2 rings)
+    static_assert(P1 % 2 == 0 && G::KS % P1 == 0, "bottleneck_tail: W2 prefetch depth");
+    bf16x8 wh[P1][TNP], wl[P1][TNP], xh[2][PM], xl[2][PM];
+#pragma unroll
+    for (int d = 0; d < P1; ++d) wload(d, wh[d], wl[d]);
     __syncthreads();  // image complete
-    read_b(0, x0h, x0l);
+    read_b(0, xh[0], xl[0]);
 #pragma unroll 1
-    for (int g = 0; g < G::KS; g += 2) {
-      read_b(g + 1, x1h, x1l);
-      mma_t(x0h, x0l, b0h, b0l);
-      wload(g + 2, b0h, b0l);
-      if (g + 2 < G::KS) read_b(g + 2, x0h, x0l);
-      mma_t(x1h, x1l, b1h, b1l);
-      wload(g + 3, b1h, b1l);
+    for (int g = 0; g < G::KS; g += P1) {
+#pragma unroll
+      for (int u = 0; u < P1; ++u) {
+        if (u + 1 < P1 || g + P1 < G::KS) read_b(g + u + 1, xh[(u + 1) & 1], xl[(u + 1) & 1]);
+        mma_t(xh[u & 1], xl[u & 1], wh[u], wl[u]);
+        wload(g + u + P1, wh[u], wl[u]);
+      }
     }
   }
 
@@ -323,38 +348,75 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
   };
   // slot q of the y2 fragments (below) holds conv3 k-step ksof(q): the wave's own k-steps
   // first, then (WN = 2) the partner's
-  auto ksof = [&](int q) { return WN == 1 ? q : (q < 2 * TN ? wn * 2 * TN + q : (1 - wn) * 2 * TN + q - 2 * TN); };
+  // (PM = 2: every slot comes back from LDS in k order)
+  auto ksof = [&](int q) {
+    return WN == 1 || PM == 2 ? q : (q < 2 * TN ? wn * 2 * TN + q : (1 - wn) * 2 * TN + q - 2 * TN);
+  };
   bf16x8 c0h[NC], c0l[NC], c1h[NC], c1l[NC];
   w3load(ksof(0), c0h, c0l);
   w3load(ksof(1), c1h, c1l);
 
   // ---- y2 = relu(acc + b2) -> conv3's A fragments (k-step 2 jj + s = registers 8 s .. 8 s + 7
-  // of channel tile jj = wn * TN + j)
+  // of channel tile jj)
   bf16x8 yh[KS3], yl[KS3];
+  if constexpr (PM == 1) {
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ch = 32 * (wn * TN + j) + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float y = fmaxf(acc[j][r] + p.b2[ch], 0.f);
-      const __bf16 hh = (__bf16)y;
-      // own k-steps sit at [0, 2 TN) of yh / yl; the partner's (WN = 2) at [2 TN, 4 TN)
-      yh[2 * j + (r >> 3)][r & 7] = hh;
-      yl[2 * j + (r >> 3)][r & 7] = (__bf16)(y - (float)hh);
+      for (int r = 0; r < 16; ++r) {
+        const int ch = 32 * (wn * TN + j) + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float y = fmaxf(acc[0][j][r] + p.b2[ch], 0.f);
+        const __bf16 hh = (__bf16)y;
+        // own k-steps sit at [0, 2 TN) of yh / yl; the partner's (WN = 2) at [2 TN, 4 TN)
+        yh[2 * j + (r >> 3)][r & 7] = hh;
+        yl[2 * j + (r >> 3)][r & 7] = (__bf16)(y - (float)hh);
+      }
+    if constexpr (WN == 2) {
+      // swap halves with the partner wave through LDS: [run][k-step][plane][64 lanes] x 16 B
+      __syncthreads();  // every wave is done reading the image
+#pragma unroll
+      for (int q = 0; q < 2 * TN; ++q) {
+        const int o = ((pr * KS3 + ksof(q)) * 2) * 1024 + lane * 16;
+        *reinterpret_cast<bf16x8*>(smem + o) = yh[q];
+        *reinterpret_cast<bf16x8*>(smem + o + 1024) = yl[q];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 2 * TN; q < KS3; ++q) {
+        const int o = ((pr * KS3 + ksof(q)) * 2) * 1024 + lane * 16;
+        yh[q] = *reinterpret_cast<const bf16x8*>(smem + o);
+        yl[q] = *reinterpret_cast<const bf16x8*>(smem + o + 1024);
+      }
     }
-  if constexpr (WN == 2) {
-    // swap halves with the partner wave through LDS: [run][k-step][plane][64 lanes] x 16 B
+  } else {
+    // every wave's (run, k-step) fragments -> LDS [run][k-step][plane][64 lanes] x 16 B;
+    // each wave then takes its phase-2 run's KS3 k-steps in order
+    static_assert(NR * KS3 * 2048 <= G::LDS, "bottleneck_tail: y2 regrouping must fit the image");
     __syncthreads();  // every wave is done reading the image
 #pragma unroll
-    for (int q = 0; q < 2 * TN; ++q) {
-      const int o = ((pr * KS3 + ksof(q)) * 2) * 1024 + lane * 16;
-      *reinterpret_cast<bf16x8*>(smem + o) = yh[q];
-      *reinterpret_cast<bf16x8*>(smem + o + 1024) = yl[q];
-    }
+    for (int i = 0; i < PM; ++i)
+#pragma unroll
+      for (int j = 0; j < TNP; ++j)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 vh, vl;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int r = 8 * s2 + e;
+            const int ch = 32 * (cg * TNP + j) + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float y = fmaxf(acc[i][j][r] + p.b2[ch], 0.f);
+            const __bf16 hh = (__bf16)y;
+            vh[e] = hh;
+            vl[e] = (__bf16)(y - (float)hh);
+          }
+          const int o = (((pg * PM + i) * KS3 + 2 * (cg * TNP + j) + s2) * 2) * 1024 + lane * 16;
+          *reinterpret_cast<bf16x8*>(smem + o) = vh;
+          *reinterpret_cast<bf16x8*>(smem + o + 1024) = vl;
+        }
     __syncthreads();
 #pragma unroll
-    for (int q = 2 * TN; q < KS3; ++q) {
-      const int o = ((pr * KS3 + ksof(q)) * 2) * 1024 + lane * 16;
+    for (int q = 0; q < KS3; ++q) {
+      const int o = ((pr * KS3 + q) * 2) * 1024 + lane * 16;
       yh[q] = *reinterpret_cast<const bf16x8*>(smem + o);
       yl[q] = *reinterpret_cast<const bf16x8*>(smem + o + 1024);
     }
@@ -560,15 +622,18 @@ void launch_conv3x3_img(const Conv3x3Args& p, int C, hipStream_t s) {
 }
 
 namespace {
-template <int C, int FB, int TB, int WN, int MINB, int NC, int NC1 = NC, int MINB1 = MINB>
+template <int C, int FB, int TB, int WN, int MINB, int NC, int NC1 = NC, int MINB1 = MINB, int PM = 1>
 void launch_tail_k(const BottleneckTailArgs& p, hipStream_t s) {
   using G = Img<C, FB, TB, WN>;
+  // W2 k-steps in flight in phase 1: 4 where the register budget (MINB) leaves room
+  constexpr int P1F = G::KS % 4 == 0 && MINB1 <= 2 ? 4 : 2, P1U = G::KS % 4 == 0 && MINB <= 2 ? 4 : 2;
   const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + TB - 1) / TB);
   if (p.w1n)
-    hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB1, NC1, true>), dim3(nblk), dim3(G::NT), G::LDS, s,
-                       p);
+    hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB1, NC1, true, P1F, PM>), dim3(nblk), dim3(G::NT), G::LDS,
+                       s, p);
   else
-    hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB, NC, false>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
+    hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB, NC, false, P1U, PM>), dim3(nblk), dim3(G::NT), G::LDS,
+                       s, p);
 }
 }  // namespace
 
@@ -593,9 +658,9 @@ void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s) {
   else if (p.w1n)
     // with the next conv1 (per-chunk barriers), two independent blocks per CU: C3 +1.5 % over the
     // 4 x 32 tile (one 102 KB block per CU)
-    launch_tail_k<128, 2, 32, 2, 2, 2, 1>(p, s);  // 64 positions, 4 waves, 70 KB image: 2 blocks / CU
+    launch_tail_k<128, 2, 32, 2, 2, 2, 1, 2, 2>(p, s);  // 64 positions, 4 waves, 70 KB image: 2 blocks / CU
   else
-    launch_tail_k<128, 4, 32, 2, 2, 2, 1>(p, s);  // 128 positions, 8 waves, 102 KB image  // 128 positions, 8 waves (2 per position run), 102 KB image
+    launch_tail_k<128, 4, 32, 2, 2, 2, 1, 2, 2>(p, s);  // 128 positions, 8 waves (2 per position run), 102 KB image
   WSP_HIP(hipGetLastError());
 }
 
