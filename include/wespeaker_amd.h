@@ -139,9 +139,11 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *                  4 = 256x128 (ResNet default), 5 = 256x256 where N % 256 == 0, else 256x128
  *                  (ECAPA-TDNN, SimAM-ResNet and HuBERT default)
  *   "res2_fused"   1 = one res2_chain launch per SE_Res2Block (default), 0 = 7 GEMMs
- *   "res2_variant" res2_chain tile (128-row windows): 0 = 2 x 2 waves, 2 = 4 waves on N with
- *                  4 W k-steps in flight (C = 128; else as 0), 3 = 8 waves (2 on M x 4 on N
- *                  for C = 128, 4 x 2 for C = 64; default)
+ *   "res2_variant" res2_chain kernel: 128-row windows with halo recompute: 0 = 2 x 2 waves,
+ *                  2 = 4 waves on N with 4 W k-steps in flight (C = 128; else as 0), 3 = 8 waves
+ *                  (2 on M x 4 on N for C = 128, 4 x 2 for C = 64; the C = 64 default);
+ *                  4 = halo-free strips of ~M / (2 x CUs) rows walked in skewed 96-row chunks
+ *                  (C = 128, default; C = 64 runs 3).  All bit-identical
  *   "astp_fused"   ECAPA-TDNN ASTP linear2 + softmax statistics in one kernel (astp_fused.hip,
  *                  default 1); 0 = linear2 GEMM + separate pooling kernel
  *   "conv3x3_img"  ResNet / SimAM-ResNet stride-1 3x3 convs from an LDS image of the input

@@ -37,9 +37,10 @@ def _pair(arch, seed, variant=0):
 @pytest.mark.parametrize("arch,B,T", [("ECAPA_TDNN_c1024", 3, 498), ("ECAPA_TDNN_c1024", 40, 498),
                                       ("ECAPA_TDNN_c512", 5, 263), ("ECAPA_TDNN_GLOB_c512", 3, 77),
                                       ("ECAPA_TDNN_GLOB_c1024", 2, 2), ("ECAPA_TDNN_c512", 7, 31)])
-@pytest.mark.parametrize("variant", [0, 2, 3])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4])
 def test_res2_fused_equals_chain_and_oracle(arch, B, T, variant):
-    """res2_variant 0: 128-row windows, 4 waves of 64 x 64; 3: 8 waves of 64 rows x 32 channels."""
+    """res2_variant 0: 128-row windows, 4 waves of 64 x 64; 3: 8 waves of 64 rows x 32 channels;
+    4: halo-free strips (c1024 widths; the c512 models run variant 3)."""
     fused, chain, sd = _pair(arch, 11, variant)
     x = torch.from_numpy(synth_feats(5, B, T, 80)).to(DEV)
     a = fused.embed(x).cpu().numpy()
@@ -52,7 +53,7 @@ def test_res2_fused_equals_chain_and_oracle(arch, B, T, variant):
     assert np.abs(a[rows] - ref.numpy()).max() < 1e-4
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4])
 def test_res2_fused_ragged_equals_chain(variant):
     fused, chain, _ = _pair("ECAPA_TDNN_c1024", 12, variant)
     frames = [3, 77, 498, 150, 2, 263, 41, 300, 9]

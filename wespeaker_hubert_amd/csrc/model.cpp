@@ -250,8 +250,9 @@ void Model::set_option(const std::string& key, int value) {
     WSP_CHECK(value >= 1 && value <= 8, "streams must be 1..8");
     impl->streams = value;
   } else if (key == "res2_variant") {
-    WSP_CHECK(value == 0 || value == 2 || value == 3,
-              "res2_variant must be 0 (4 waves, 2 x 2), 2 (4 waves on N, 4 W k-steps in flight) or 3 (8 waves)");
+    WSP_CHECK(value == 0 || value == 2 || value == 3 || value == 4,
+              "res2_variant must be 0 (4 waves, 2 x 2), 2 (4 waves on N, 4 W k-steps in flight), 3 (8 waves) "
+              "or 4 (halo-free strips, c1024 widths; else as 3)");
     impl->res2_variant = value;
   } else if (key == "x3_variant") {
     WSP_CHECK(value == 3 || value == 4 || value == 5, "x3_variant must be 3, 4 or 5");

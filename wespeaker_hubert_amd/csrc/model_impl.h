@@ -150,7 +150,7 @@ struct Model::Impl {
   // next block's conv1 on the tail's output while it is on chip, 2 = the tail alone, 0 = off
   int res_tail = 1;
   bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
-  int res2_variant = 3;  // res2_chain.hip kernel variant (option "res2_variant"; 3 = 8 waves, measured fastest)
+  int res2_variant = 4;  // res2_chain.hip kernel variant (option "res2_variant"; 4 = halo-free strips, C2 1.48 -> 1.24 ms/step; c512 widths run 3)
   ConvW conv, pool1, pool2;
   // conv_cat on [out2, out3, g4 * h3_4]: out4 = out3 + g4 * h3_4, so W . [out2; out3; out4]
   // = W_a out2 + (W_b + W_c) out3 + W_c (g4 * h3_4) — the last SE block's residual pass
@@ -1151,14 +1151,14 @@ struct Model::Impl {
         r.M = M;
         r.T = T;
         r.dil = dil;
-        r.rout = res2_chain_rout(dil, res2_variant);
+        r.rout = res2_chain_rout(dil, w == 128 ? res2_variant : std::min(res2_variant, 3), M);
         r.seg = seg;
         r.nseg = B;
         r.w = b.r2w;
         r.bias = b.r2b;
         r.scale = b.r2s;
         r.shift = b.r2t;
-        r.variant = res2_variant;
+        r.variant = w == 128 ? res2_variant : std::min(res2_variant, 3);
         run("res2_k3", 7 * 2.0 * M * w * 3 * w, s, [&] { launch_res2_chain(r, w, s); });
       }
       for (int i = 0; i < 7 && !(precision == 1 && res2_fused && b.r2w); ++i) {

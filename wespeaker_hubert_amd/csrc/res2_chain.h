@@ -20,10 +20,10 @@ struct Res2Args {
   const float* bias;
   const float* scale;
   const float* shift;
-  int variant;  // 0: 128-row windows, two blocks per CU (default); 1: 256-row windows
+  int variant;  // 0 / 2 / 3: 128-row windows (halo recompute); 4: strips (w = 128, else as 3)
 };
 bool res2_chain_supported(int w, int dil);
-int res2_chain_rout(int dil, int variant);  // output rows per block
+int res2_chain_rout(int dil, int variant, int M);  // output rows per block
 void launch_res2_chain(const Res2Args& p, int w, hipStream_t s);
 
 }  // namespace wsp

@@ -34,6 +34,9 @@
 //     term dominates; the rest is the per-step barriers and image rewrite.
 // HBM traffic per row: spx[0..6] read once (+ halo re-reads, mostly L2 hits of
 // the neighbouring block) and sp_0..6 written once.
+#include <algorithm>
+#include <type_traits>
+
 #include "gemm_common.h"
 #include "res2_chain.h"
 
@@ -286,6 +289,280 @@ __global__ __launch_bounds__(NWv * 64, R == 128 ? NWv / 2 : 1) void res2_chain_k
   }
 }
 
+
+// ---- variant 4: halo-free strips (skewed chunk pipeline), W = 128 ----------
+// A block owns a strip of `rout` consecutive frame rows (about M / (2 x CUs):
+// one round of two blocks per CU) and walks it in chunks of kSR = 96 rows.  In
+// chunk c, conv i computes the rows [r0 + c*kSR - i*d, ... + kSR): each conv lags
+// the previous one by d rows, so the rows it needs of X_i = sp_{i-1} + spx[i]
+// are the kSR rows conv i-1 has just produced plus 2d rows from the previous
+// chunk (kept in LDS: the last 2d image rows of X_i are saved as the image is
+// overwritten, and copied back in front of the next chunk's X_i).  The chain's
+// receptive field costs 6d warm-up rows at the start of a strip and 6d drain rows
+// at its end — 12d per ~250-row strip instead of 12d per 128-row window — and one
+// round of blocks instead of 3-4 rounds of windows.  Same operands, k order and
+// epilogue as the other variants, so the owned rows are bit-identical.
+constexpr int kSR = 96;                            // output rows per chunk (3 tiles of 32)
+constexpr int kSIR = kSR + 2 * kPad;               // image rows: 2d history + kSR new
+constexpr int kSRB = 256;                          // bytes per image row and plane (128 bf16)
+constexpr int kSPlane = (kSIR + 1) * kSRB;         // + the zero row
+constexpr int kSHistRows = 2 * kPad;               // history rows per slot
+constexpr int kSLds = 2 * kSPlane + 6 * kSHistRows * 2 * kSRB;  // image + 6 history slots (X_1..X_6)
+static_assert(kSR % 16 == 0, "history rows keep their swizzle only if kSR % 16 == 0");
+static_assert(2 * kSLds <= 160 * 1024, "two strip blocks per CU");
+
+__device__ __forceinline__ int s_off(int ir, int ch) { return ((((ch >> 3) ^ (ir & 15)) << 4)) + (ch & 7) * 2; }
+
+template <int PD>
+__global__ __launch_bounds__(256, 2) void res2_strip_kernel(const Res2Args p) {
+  constexpr int W = 128, KS = 3 * W / 16, KC = W / 16, TM = 3, kTotal = 7 * KS;
+  static_assert(KS % PD == 0 && PD % 2 == 0, "res2 strip W prefetch depth");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* xhi = smem;
+  unsigned char* xlo = smem + kSPlane;
+  unsigned char* hist = smem + 2 * kSPlane;  // [slot 6][row 2kPad][plane 2][kSRB]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wn = tid >> 6;  // 4 waves, 32 output channels each
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+  const int d = p.dil;
+  const int M = p.M;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring strips share an XCD L2
+  const int own0 = blk * p.rout;
+  const int own1 = min(own0 + p.rout, M);
+  const int r0 = own0 - 6 * d;  // chunk 0's first conv-0 output row
+  const int nch = (own1 - own0 + 12 * d + kSR - 1) / kSR;
+
+  // ---- zero row, zeroed history, X_0 of chunk 0: image row ir = frame row r0 - d + ir
+  if (tid < kSRB / 4) {
+    reinterpret_cast<unsigned*>(xhi + kSIR * kSRB)[tid] = 0u;
+    reinterpret_cast<unsigned*>(xlo + kSIR * kSRB)[tid] = 0u;
+  }
+  for (int q = tid; q < 6 * kSHistRows * 2 * kSRB / 16; q += 256)
+    reinterpret_cast<u32x4*>(hist)[q] = u32x4{0u, 0u, 0u, 0u};
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x);
+  auto put4 = [&](int ir, int c, const f32x4& v) {
+    bf16x4 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const __bf16 hh = (__bf16)v[e];
+      hi[e] = hh;
+      lo[e] = (__bf16)(v[e] - (float)hh);
+    }
+    const int a = ir * kSRB + s_off(ir, c);
+    *reinterpret_cast<bf16x4*>(xhi + a) = hi;
+    *reinterpret_cast<bf16x4*>(xlo + a) = lo;
+  };
+  for (int q = tid; q < (kSR + 2 * d) * (W / 4); q += 256) {
+    const int ir = q / (W / 4);
+    const int c = (q - ir * (W / 4)) * 4;
+    const int m = r0 - d + ir;
+    put4(ir, c, bload4(rx, (m >= 0 && m < M) ? (m * p.ldx + c) * 4 : kOOB));
+  }
+
+  // ---- W fragments from global: k-step g (0 .. 7*KS-1, wrapping across chunks),
+  // plane pl, column tile wn at ((g * 2 + pl) * (W / 32) + wn) * 1 KB + lane * 16
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w);
+  const int wlane = (wn * 64 + lane) * 16;
+  auto wload = [&](int g, bf16x8& bh, bf16x8& bl) {
+    const int o = g * 2 * (W / 32) * 1024 + wlane;
+    bh = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, o, 0, 0));
+    bl = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, o + (W / 32) * 1024, 0, 0));
+  };
+  bf16x8 wbh[PD], wbl[PD];
+#pragma unroll
+  for (int u = 0; u < PD; ++u) wload(u, wbh[u], wbl[u]);
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(p.out);
+  f32x16 acc[TM];
+  // A-fragment row of tile i for tap j: image row i*32 + r32 + j*d when bit j of
+  // vm[i] says the tap stays inside the row's utterance, else the zero row (computed,
+  // not looked up: a tap-indexed array would live in scratch)
+  int vm[TM];
+  int dq = d;
+  // NA = active tiles (the last chunk of a strip may need fewer than TM)
+  auto read_a = [&](auto na, int t, bf16x8 (&ah)[TM], bf16x8 (&al)[TM]) {
+    constexpr int NA = decltype(na)::value;
+    const int tap = t / KC, q = (t % KC) * 2 + h;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int ir = ((vm[i] >> tap) & 1) ? i * 32 + r32 + tap * dq : kSIR;
+      const int a = ir * kSRB + ((q ^ (ir & 15)) << 4);
+      ah[i] = *reinterpret_cast<const bf16x8*>(xhi + a);
+      al[i] = *reinterpret_cast<const bf16x8*>(xlo + a);
+    }
+  };
+  // one 16-deep k-step g; its ring slot then reloads k-step g + PD (mod 7*KS: the
+  // next chunk's conv 0 follows conv 6)
+  auto mma = [&](auto na, int g, const bf16x8 (&ah)[TM], const bf16x8 (&al)[TM], bf16x8& bh, bf16x8& bl) {
+    constexpr int NA = decltype(na)::value;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, acc[i], 0, 0, 0);
+    }
+    const int gn = g + PD;
+    wload(gn >= kTotal ? gn - kTotal : gn, bh, bl);
+  };
+  bf16x8 ah2[2][TM], al2[2][TM];
+  const int col = wn * 32 + r32;
+
+  // one conv of one chunk on its NA active 32-row tiles
+  auto conv_step = [&](auto na, int c, int step, bool more) {
+    constexpr int NA = decltype(na)::value;
+        const int base = r0 + c * kSR - step * d;  // frame row of this conv's output row 0
+        // per step: keeps hipcc from hoisting the 48 d-dependent image addresses of the
+        // epilogue (and the fragment rows) out of the loops into spilled registers
+        dq = d;
+        asm volatile("" : "+s"(dq));
+        // A-fragment rows of this lane per tile and tap: image row lr + j*d, or the zero
+        // row when the tap leaves the row's utterance (or the row is outside the batch)
+  #pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int lr = i * 32 + r32;
+          const int m = base + lr;
+          int t = -1, L = 0;
+          if (m >= 0 && m < M) {
+            if (p.seg) {
+              const int u = seg_of(p.seg, p.nseg, m);
+              t = m - p.seg[u];
+              L = p.seg[u + 1] - p.seg[u];
+            } else {
+              const int u = m / p.T;
+              t = m - u * p.T;
+              L = p.T;
+            }
+          }
+          int v = 0;
+  #pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const int tt = t + (j - 1) * d;
+            v |= (t >= 0 && tt >= 0 && tt < L) ? 1 << j : 0;
+          }
+          vm[i] = v;
+        }
+  #pragma unroll
+        for (int i = 0; i < NA; ++i)
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+        const int gb = step * KS;
+        read_a(na, 0, ah2[0], al2[0]);
+  #pragma unroll 1
+        for (int t = 0; t < KS - PD; t += PD) {
+  #pragma unroll
+          for (int u = 0; u < PD; ++u) {
+            read_a(na, t + u + 1, ah2[(u + 1) & 1], al2[(u + 1) & 1]);
+            mma(na, gb + t + u, ah2[u & 1], al2[u & 1], wbh[u], wbl[u]);
+          }
+        }
+        // next image rows' addend, issued PD k-steps before the epilogue: spx[step + 1]
+        // on this conv's rows, or (after conv 6) spx[0] on the next chunk's new rows
+        const bool wimg = step < 6 || more;
+        int ldx4 = p.ldx * 4, ldo4 = p.ldo * 4;
+        int abase = step < 6 ? base : r0 + (c + 1) * kSR + d;
+        asm volatile("" : "+s"(ldx4), "+s"(ldo4), "+s"(abase));
+        const int acol = step < 6 ? (step + 1) * W : 0;
+        float nx[TM][16];
+        f32x4 xh = {0.f, 0.f, 0.f, 0.f};
+        if (wimg) {
+  #pragma unroll
+          for (int i = 0; i < NA; ++i) {
+            const int m0 = abase + i * 32 + 4 * h;  // row of register 0
+            const int lo = -m0, hi = M - m0;
+            const int b0 = (m0 * p.ldx + acol + col) * 4;
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rr = (r & 3) + 8 * (r >> 2);
+              nx[i][r] = __builtin_bit_cast(
+                  float, __builtin_amdgcn_raw_buffer_load_b32(rx, (rr >= lo && rr < hi) ? b0 + rr * ldx4 : kOOB, 0, 0));
+            }
+          }
+          if (step == 6 && tid < 2 * d * (W / 4)) {  // the next chunk's X_0 history rows
+            const int k = tid / (W / 4), c4 = (tid - k * (W / 4)) * 4;
+            const int m = r0 + (c + 1) * kSR - d + k;
+            xh = bload4(rx, (m >= 0 && m < M) ? (m * p.ldx + c4) * 4 : kOOB);
+          }
+        }
+  #pragma unroll
+        for (int u = 0; u < PD; ++u) {
+          if (u + 1 < PD) read_a(na, KS - PD + u + 1, ah2[(u + 1) & 1], al2[(u + 1) & 1]);
+          mma(na, gb + KS - PD + u, ah2[u & 1], al2[u & 1], wbh[u], wbl[u]);
+        }
+        __syncthreads();  // every wave is done reading X_step
+
+        // ---- epilogue: sp = BN(ReLU(acc + b)); owned rows -> out; X_{step+1} (or the
+        // next chunk's X_0) -> image rows [2d, 2d + kSR); X_step's last 2d rows -> history
+        const float bv = p.bias[step * W + col];
+        const float sc = p.scale[step * W + col];
+        const float sh = p.shift[step * W + col];
+        const int cp = col & ~1;
+        unsigned char* hslot = hist + (step - 1) * (kSHistRows * 2 * kSRB);  // X_step's slot (step >= 1)
+  #pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int lr0 = i * 32 + 4 * h;
+          const int m0 = base + lr0;
+          const int olo = own0 - m0, ohi = own1 - m0;
+          const int b0 = (m0 * p.ldo + step * W + col) * 4;
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rr = (r & 3) + 8 * (r >> 2);
+            const float y = fmaxf(acc[i][r] + bv, 0.f) * sc + sh;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rout,
+                                                  (rr >= olo && rr < ohi) ? b0 + rr * ldo4 : kOOB, 0, 0);
+            if (wimg) {
+              const float x = step < 6 ? y + nx[i][r] : nx[i][r];
+              const __bf16 hh = (__bf16)x;
+              const __bf16 ll = (__bf16)(x - (float)hh);
+              // lanes l, l^1 hold channels col, col^1 of this row: the even lane writes
+              // both hi halves, the odd lane both lo halves (one 4-B store each)
+              const unsigned send = (lane & 1) ? bf_bits(hh) : bf_bits(ll);
+              const unsigned recv = (unsigned)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
+              const int ir = 2 * dq + lr0 + rr;
+              const int o = s_off(ir, cp);
+              unsigned char* img = (lane & 1) ? xlo : xhi;
+              unsigned* dst = reinterpret_cast<unsigned*>(img + ir * kSRB + o);
+              if (NA == TM && i == TM - 1 && step >= 1 && ir >= kSR) {  // X_step's rows [kSR, kSR + 2d): save before overwriting
+                *reinterpret_cast<unsigned*>(hslot + ((ir - kSR) * 2 + (lane & 1)) * kSRB + o) = *dst;
+              }
+              *dst = (lane & 1) ? (recv | ((unsigned)bf_bits(ll) << 16)) : ((unsigned)bf_bits(hh) | (recv << 16));
+            }
+          }
+        }
+        // image rows [0, 2d): X_{step+1}'s history from the previous chunk (slot step),
+        // or the next chunk's X_0 rows fetched above
+        if (step < 6) {
+          if (tid < 2 * d * 32) {  // 16-B pieces: row k, plane pl, piece e
+            const int k = tid >> 5, pl = (tid >> 4) & 1, e = tid & 15;
+            const u32x4 v = reinterpret_cast<const u32x4*>(hist + step * (kSHistRows * 2 * kSRB) + (k * 2 + pl) * kSRB)[e];
+            reinterpret_cast<u32x4*>((pl ? xlo : xhi) + k * kSRB)[e] = v;
+          }
+        } else if (more && tid < 2 * d * (W / 4)) {
+          const int k = tid / (W / 4), c4 = (tid - k * (W / 4)) * 4;
+          put4(k, c4, xh);
+        }
+  };
+
+  // the last chunk needs only the rows up to the strip's end (+ the 6d drain rows
+  // of conv 6): its inactive tiles are skipped (their image rows are never read)
+  const int last_tiles = (own1 - own0 + 12 * d - (nch - 1) * kSR + 31) / 32;
+#pragma unroll 1
+  for (int c = 0; c < nch; ++c) {
+    const bool more = c + 1 < nch;
+    const int nt = more ? TM : last_tiles;
+#pragma unroll 1
+    for (int step = 0; step < 7; ++step) {
+      if (nt >= 3) conv_step(std::integral_constant<int, 3>{}, c, step, more);
+      else if (nt == 2) conv_step(std::integral_constant<int, 2>{}, c, step, more);
+      else conv_step(std::integral_constant<int, 1>{}, c, step, more);
+      __syncthreads();  // the next conv's image is complete
+    }
+  }
+}
+
 }  // namespace
 
 bool res2_chain_supported(int w, int dil) { return (w == 64 || w == 128) && dil >= 1 && dil <= kPad; }
@@ -300,7 +577,9 @@ void launch_res2_k(const Res2Args& p, int nblk, hipStream_t s) {
 
 template <int W>
 void launch_res2_w(const Res2Args& p, int nblk, hipStream_t s) {
-  if (p.variant == 3) {
+  if (W == 128 && p.variant == 4) {
+    hipLaunchKernelGGL(res2_strip_kernel<4>, dim3(nblk), dim3(256), kSLds, s, p);
+  } else if (p.variant == 3) {
     if constexpr (W == 128) launch_res2_k<W, 128, 4, 8>(p, nblk, s);  // 8 waves of 64 rows x 32 channels
     else launch_res2_k<W, 128, 2, 8>(p, nblk, s);
   } else if (p.variant == 2) {
@@ -314,7 +593,7 @@ void launch_res2_w(const Res2Args& p, int nblk, hipStream_t s) {
 void launch_res2_chain(const Res2Args& p, int w, hipStream_t s) {
   WSP_CHECK(res2_chain_supported(w, p.dil), "res2_chain: width must be 64 or 128 and dilation 1..4");
   WSP_CHECK(p.M > 0 && (p.seg || p.T > 0), "res2_chain: empty shape");
-  WSP_CHECK(p.rout == res2_chain_rout(p.dil, p.variant), "res2_chain: rout must be res2_chain_rout(dil, variant)");
+  WSP_CHECK(p.rout == res2_chain_rout(p.dil, p.variant, p.M), "res2_chain: rout must be res2_chain_rout(dil, variant, M)");
   WSP_CHECK((long long)p.M * p.ldx * 4 < (long long)kOOB && (long long)p.M * p.ldo * 4 < (long long)kOOB,
             "res2_chain: operand exceeds 2 GiB (split the batch)");
   WSP_CHECK(p.ldx >= 8 * w && p.ldo >= 7 * w && p.ldx % 4 == 0, "res2_chain: bad leading dimensions");
@@ -326,6 +605,22 @@ void launch_res2_chain(const Res2Args& p, int w, hipStream_t s) {
   WSP_HIP(hipGetLastError());
 }
 
-int res2_chain_rout(int dil, int variant) { return res2_rows(variant) - 12 * dil; }
+// Strips (variant 4, W = 128): one round of two blocks per CU over the batch's rows,
+// at least 64 rows per strip (the 12d warm-up / drain rows are per strip).
+static int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    WSP_HIP(hipGetDevice(&dev));
+    WSP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+int res2_chain_rout(int dil, int variant, int M) {
+  if (variant == 4) return std::max(64, ceil_div(M, 2 * device_cus()));
+  return res2_rows(variant) - 12 * dil;
+}
 
 }  // namespace wsp
