@@ -394,6 +394,7 @@ __global__ __launch_bounds__(256, 2) void res2_strip_kernel(const Res2Args p) {
       ah[i] = *reinterpret_cast<const bf16x8*>(xhi + a);
       al[i] = *reinterpret_cast<const bf16x8*>(xlo + a);
     }
+    __builtin_amdgcn_sched_barrier(0);  // k-step t's fragment reads go out before k-step t-1's MFMAs
   };
   // one 16-deep k-step g; its ring slot then reloads k-step g + PD (mod 7*KS: the
   // next chunk's conv 0 follows conv 6)
@@ -407,6 +408,9 @@ __global__ __launch_bounds__(256, 2) void res2_strip_kernel(const Res2Args p) {
     }
     const int gn = g + PD;
     wload(gn >= kTotal ? gn - kTotal : gn, bh, bl);
+    // keep the slot's reload right behind its MFMAs (hipcc otherwise sinks the whole
+    // group's loads to the end of the unrolled group: the ring would hide nothing)
+    __builtin_amdgcn_sched_barrier(0);
   };
   bf16x8 ah2[2][TM], al2[2][TM];
   const int col = wn * 32 + r32;
