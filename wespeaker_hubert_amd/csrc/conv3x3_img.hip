@@ -161,12 +161,19 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void conv3x3_img_kernel(cons
   read_a(0, a0h, a0l);
 #pragma unroll 1
   for (int g = 0; g < G::KS; g += 2) {
+    // scheduling fences: the next k-step's fragment reads go out before this k-step's
+    // MFMAs and each ring slot's reload right behind them (hipcc otherwise sinks the
+    // loads to the end of the loop body and waits on the reads right after issuing them)
     read_a(g + 1, a1h, a1l);
+    __builtin_amdgcn_sched_barrier(0);
     mma(a0h, a0l, b0h, b0l);
     wload(g + 2, b0h, b0l);
+    __builtin_amdgcn_sched_barrier(0);
     if (g + 2 < G::KS) read_a(g + 2, a0h, a0l);
+    __builtin_amdgcn_sched_barrier(0);
     mma(a1h, a1l, b1h, b1l);
     wload(g + 3, b1h, b1l);
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   // ---- epilogue (conv_gemm_x3's: y = act(acc + bias (+ res)) * scale + shift)
@@ -326,9 +333,12 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
     for (int g = 0; g < G::KS; g += P1) {
 #pragma unroll
       for (int u = 0; u < P1; ++u) {
+        // fences as in conv3x3_img_kernel: reads one k-step ahead, reloads behind their MFMAs
         if (u + 1 < P1 || g + P1 < G::KS) read_b(g + u + 1, xh[(u + 1) & 1], xl[(u + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
         mma_t(xh[u & 1], xl[u & 1], wh[u], wl[u]);
         wload(g + u + P1, wh[u], wl[u]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -498,6 +508,7 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
         const int qn = q + 2 < KS3 ? q + 2 : 0;
         w3load((q + 2 < KS3 ? chunk : chunk + 1) * KS3 + ksof(qn), c0h, c0l);
       }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < NC; ++j) {
         a3[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(yl[q + 1], c1h[j], a3[j], 0, 0, 0);
@@ -508,6 +519,7 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
         const int qn = q + 3 < KS3 ? q + 3 : 1;
         w3load((q + 3 < KS3 ? chunk : chunk + 1) * KS3 + ksof(qn), c1h, c1l);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     // epilogue: y = relu(acc + b3 + res), conv3x3_img's store pattern over 4C channels
 #pragma unroll
@@ -554,6 +566,7 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
           acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, u0h[j], acc1[j], 0, 0, 0);
         }
         if (kk + 2 < KK) w1load(chunk, kk + 2, u0h, u0l);
+        __builtin_amdgcn_sched_barrier(0);
         {
           const int a = cbaddr(pr * 32 + r32, 2 * (kk + 1) + h);
           ah = *reinterpret_cast<const bf16x8*>(cbhi + a);
@@ -566,6 +579,7 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
           acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, u1h[j], acc1[j], 0, 0, 0);
         }
         if (kk + 3 < KK) w1load(chunk, kk + 3, u1h, u1l);
+        __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (!CB2) __syncthreads();  // the chunk buffer is rewritten by the next chunk
     }
