@@ -377,6 +377,9 @@ __global__ __launch_bounds__(256, 2) void res2_strip_kernel(const Res2Args p) {
   __syncthreads();
 
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(p.out);
+  const __amdgpu_buffer_rsrc_t rbias = make_rsrc(p.bias);
+  const __amdgpu_buffer_rsrc_t rscale = make_rsrc(p.scale);
+  const __amdgpu_buffer_rsrc_t rshift = make_rsrc(p.shift);
   f32x16 acc[TM];
   // A-fragment row of tile i for tap j: image row i*32 + r32 + j*d when bit j of
   // vm[i] says the tap stays inside the row's utterance, else the zero row (computed,
@@ -454,6 +457,10 @@ __global__ __launch_bounds__(256, 2) void res2_strip_kernel(const Res2Args p) {
   #pragma unroll
           for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
         const int gb = step * KS;
+        // this conv's epilogue constants, fetched now (they land during the k-loop)
+        const float bv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbias, (step * W + col) * 4, 0, 0));
+        const float sc = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rscale, (step * W + col) * 4, 0, 0));
+        const float sh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rshift, (step * W + col) * 4, 0, 0));
         read_a(na, 0, ah2[0], al2[0]);
   #pragma unroll 1
         for (int t = 0; t < KS - PD; t += PD) {
@@ -500,42 +507,51 @@ __global__ __launch_bounds__(256, 2) void res2_strip_kernel(const Res2Args p) {
 
         // ---- epilogue: sp = BN(ReLU(acc + b)); owned rows -> out; X_{step+1} (or the
         // next chunk's X_0) -> image rows [2d, 2d + kSR); X_step's last 2d rows -> history
-        const float bv = p.bias[step * W + col];
-        const float sc = p.scale[step * W + col];
-        const float sh = p.shift[step * W + col];
         const int cp = col & ~1;
         unsigned char* hslot = hist + (step - 1) * (kSHistRows * 2 * kSRB);  // X_step's slot (step >= 1)
-  #pragma unroll
-        for (int i = 0; i < NA; ++i) {
-          const int lr0 = i * 32 + 4 * h;
-          const int m0 = base + lr0;
-          const int olo = own0 - m0, ohi = own1 - m0;
-          const int b0 = (m0 * p.ldo + step * W + col) * 4;
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rr = (r & 3) + 8 * (r >> 2);
-            const float y = fmaxf(acc[i][r] + bv, 0.f) * sc + sh;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rout,
-                                                  (rr >= olo && rr < ohi) ? b0 + rr * ldo4 : kOOB, 0, 0);
-            if (wimg) {
-              const float x = step < 6 ? y + nx[i][r] : nx[i][r];
-              const __bf16 hh = (__bf16)x;
-              const __bf16 ll = (__bf16)(x - (float)hh);
-              // lanes l, l^1 hold channels col, col^1 of this row: the even lane writes
-              // both hi halves, the odd lane both lo halves (one 4-B store each)
-              const unsigned send = (lane & 1) ? bf_bits(hh) : bf_bits(ll);
-              const unsigned recv = (unsigned)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
-              const int ir = 2 * dq + lr0 + rr;
-              const int o = s_off(ir, cp);
-              unsigned char* img = (lane & 1) ? xlo : xhi;
-              unsigned* dst = reinterpret_cast<unsigned*>(img + ir * kSRB + o);
-              if (NA == TM && i == TM - 1 && step >= 1 && ir >= kSR) {  // X_step's rows [kSR, kSR + 2d): save before overwriting
-                *reinterpret_cast<unsigned*>(hslot + ((ir - kSR) * 2 + (lane & 1)) * kSRB + o) = *dst;
+        // MODE 0: stores only (the strip's last conv 6); 1: X_{step+1} = sp + spx[step+1];
+        // 2: the next chunk's X_0 = spx[0].  FULL: every row of the chunk is owned (no
+        // per-row bounds).  Uniform choices hoisted out of the 48-register loop.
+        auto epi = [&](auto mode_, auto full_) {
+          constexpr int MODE = decltype(mode_)::value;
+          constexpr bool FULL = decltype(full_)::value;
+#pragma unroll
+          for (int i = 0; i < NA; ++i) {
+            const int lr0 = i * 32 + 4 * h;
+            const int m0 = base + lr0;
+            const int olo = own0 - m0, ohi = own1 - m0;
+            const int b0 = (m0 * p.ldo + step * W + col) * 4;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rr = (r & 3) + 8 * (r >> 2);
+              const float y = fmaxf(acc[i][r] + bv, 0.f) * sc + sh;
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rout,
+                                                    (FULL || (rr >= olo && rr < ohi)) ? b0 + rr * ldo4 : kOOB, 0, 0);
+              if constexpr (MODE != 0) {
+                const float x = MODE == 1 ? y + nx[i][r] : nx[i][r];
+                const __bf16 hh = (__bf16)x;
+                const __bf16 ll = (__bf16)(x - (float)hh);
+                // lanes l, l^1 hold channels col, col^1 of this row: the even lane writes
+                // both hi halves, the odd lane both lo halves (one 4-B store each)
+                const unsigned send = (lane & 1) ? bf_bits(hh) : bf_bits(ll);
+                const unsigned recv = (unsigned)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
+                const int ir = 2 * dq + lr0 + rr;
+                const int o = s_off(ir, cp);
+                unsigned char* img = (lane & 1) ? xlo : xhi;
+                unsigned* dst = reinterpret_cast<unsigned*>(img + ir * kSRB + o);
+                if (NA == TM && i == TM - 1 && ir >= kSR) {  // X_step's rows [kSR, kSR + 2d): save before overwriting
+                  if (step >= 1) *reinterpret_cast<unsigned*>(hslot + ((ir - kSR) * 2 + (lane & 1)) * kSRB + o) = *dst;
+                }
+                *dst = (lane & 1) ? (recv | ((unsigned)bf_bits(ll) << 16)) : ((unsigned)bf_bits(hh) | (recv << 16));
               }
-              *dst = (lane & 1) ? (recv | ((unsigned)bf_bits(ll) << 16)) : ((unsigned)bf_bits(hh) | (recv << 16));
             }
           }
-        }
+        };
+        const bool full = base >= own0 && base + NA * 32 <= own1;
+        if (!wimg) epi(std::integral_constant<int, 0>{}, std::false_type{});
+        else if (step == 6) epi(std::integral_constant<int, 2>{}, std::false_type{});
+        else if (full) epi(std::integral_constant<int, 1>{}, std::true_type{});
+        else epi(std::integral_constant<int, 1>{}, std::false_type{});
         // image rows [0, 2d): X_{step+1}'s history from the previous chunk (slot step),
         // or the next chunk's X_0 rows fetched above
         if (step < 6) {
