@@ -305,7 +305,9 @@ __global__ __launch_bounds__(NWv * 64, R == 128 ? NWv / 2 : 1) void res2_chain_k
 constexpr int kSR = 96;                            // output rows per chunk (3 tiles of 32)
 constexpr int kSIR = kSR + 2 * kPad;               // image rows: 2d history + kSR new
 constexpr int kSRB = 256;                          // bytes per image row and plane (128 bf16)
-constexpr int kSPlane = (kSIR + 1) * kSRB;         // + the zero row
+// + the zero row; + 64 B so the lo plane sits 16 banks after the hi plane (the epilogue's
+// paired hi / lo 4-B stores of one row then hit distinct banks)
+constexpr int kSPlane = (kSIR + 1) * kSRB + 64;
 constexpr int kSHistRows = 2 * kPad;               // history rows per slot
 constexpr int kSLds = 2 * kSPlane + 6 * kSHistRows * 2 * kSRB;  // image + 6 history slots (X_1..X_6)
 static_assert(kSR % 16 == 0, "history rows keep their swizzle only if kSR % 16 == 0");
