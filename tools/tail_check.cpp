@@ -1,0 +1,122 @@
+// Bottleneck-tail kernel check + timing (development tool, not part of the product):
+// launch_bottleneck_tail with the next conv1 fused, variant 1 (bottleneck_tail_kernel)
+// against variant 3 (tail2_kernel) on random operands; prints max |diff| of the block
+// output and of y1', the first mismatching position, and the average launch time.
+//   tail_check C B F T [reps]
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../wespeaker_hubert_amd/csrc/conv3x3_img.h"
+
+using namespace wsp;
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      std::exit(1);                                                                \
+    }                                                                              \
+  } while (0)
+
+static uint16_t f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+template <typename T>
+static T* dev(const std::vector<T>& h) {
+  T* d;
+  CK(hipMalloc(&d, h.size() * sizeof(T)));
+  CK(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return d;
+}
+
+int main(int argc, char** argv) {
+  const int C = argc > 1 ? std::atoi(argv[1]) : 128;
+  const int B = argc > 2 ? std::atoi(argv[2]) : 1;
+  const int F = argc > 3 ? std::atoi(argv[3]) : 20;
+  const int T = argc > 4 ? std::atoi(argv[4]) : 70;
+  const int reps = argc > 5 ? std::atoi(argv[5]) : 20;
+  std::mt19937 rng(7);
+  std::uniform_real_distribution<float> u01(0.f, 1.f);
+  std::normal_distribution<float> nw(0.f, 0.05f);
+  const size_t npos = (size_t)B * F * T;
+  std::vector<float> y1(npos * C), res(npos * 4 * C), b2(C), b3(4 * C), b1(C);
+  for (auto& v : y1) v = u01(rng);
+  for (auto& v : res) v = u01(rng) - 0.5f;
+  for (auto& v : b2) v = nw(rng);
+  for (auto& v : b3) v = nw(rng);
+  for (auto& v : b1) v = nw(rng);
+  auto frag = [&](size_t n) {  // hi images random, lo images random small
+    std::vector<uint16_t> w(n);
+    for (auto& x : w) x = f2bf(nw(rng));
+    return w;
+  };
+  const std::vector<uint16_t> w2 = frag((size_t)9 * C / 16 * 2 * (C / 32) * 512);
+  const std::vector<uint16_t> w3 = frag((size_t)C / 16 * 2 * (4 * C / 32) * 512);
+  const std::vector<uint16_t> w1 = frag((size_t)4 * C / 16 * 2 * (C / 32) * 512);
+  float *dy1 = dev(y1), *dres = dev(res), *db2 = dev(b2), *db3 = dev(b3), *db1 = dev(b1);
+  uint16_t *dw2 = dev(w2), *dw3 = dev(w3), *dw1 = dev(w1);
+  float *out[2], *y1n[2];
+  for (int i = 0; i < 2; ++i) {
+    CK(hipMalloc(&out[i], npos * 4 * C * 4));
+    CK(hipMalloc(&y1n[i], npos * C * 4));
+    CK(hipMemset(out[i], 0xFF, npos * 4 * C * 4));
+    CK(hipMemset(y1n[i], 0xFF, npos * C * 4));
+  }
+  const int vars[2] = {1, 3};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int i = 0; i < 2; ++i) {
+    BottleneckTailArgs a{dy1, dres, out[i], B, F, T, dw2, db2, dw3, db3};
+    a.w1n = dw1;
+    a.b1n = db1;
+    a.y1n = y1n[i];
+    a.variant = vars[i];
+    launch_bottleneck_tail(a, C, 0);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0, 0));
+    for (int r = 0; r < reps; ++r) launch_bottleneck_tail(a, C, 0);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::printf("variant %d: %.4f ms per launch\n", vars[i], ms / reps);
+  }
+  auto cmp = [&](const char* name, float* const* d, size_t n, int ch) {
+    std::vector<float> h0(n), h1(n);
+    CK(hipMemcpy(h0.data(), d[0], n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(h1.data(), d[1], n * 4, hipMemcpyDeviceToHost));
+    double mx = 0, ref = 0;
+    long first = -1;
+    for (size_t i = 0; i < n; ++i) {
+      const double df = std::fabs((double)h0[i] - h1[i]);
+      ref = std::fmax(ref, std::fabs((double)h0[i]));
+      if (!(df <= 1e-4 * std::fmax(1.0, std::fabs((double)h0[i])))) {
+        if (first < 0) first = (long)i;
+      }
+      if (!(df <= mx)) mx = df;
+    }
+    std::printf("%s: max |diff| %.3g (max |ref| %.3g)", name, mx, ref);
+    if (first >= 0) {
+      const long pos = first / ch, c = first % ch;
+      const long b = pos / ((long)F * T), rem = pos % ((long)F * T);
+      std::printf("  first mismatch b %ld f %ld t %ld c %ld: %g vs %g", b, rem / T, rem % T, c, h0[first],
+                  h1[first]);
+    }
+    std::printf("\n");
+  };
+  cmp("out", out, npos * 4 * C, 4 * C);
+  cmp("y1n", y1n, npos * C, C);
+  return 0;
+}

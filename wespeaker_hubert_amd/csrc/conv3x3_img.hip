@@ -602,6 +602,310 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
   }
 }
 
+// Bottleneck tail with the next conv1 fused, every wave on TWO position runs in both phases
+// (option res_tail 3, r3; 64 / 128 planes).  bottleneck_tail_kernel's fused forms fetch, per
+// chunk and wave, W3 / W1 fragments that feed one 32-position run (and for 64 planes also
+// conv2's W2); here each of the 4 waves runs conv2, conv3 and the next conv1 for a PAIR of runs
+// and 1 / GW of the columns, so every weight fragment fetched from L2 feeds two MFMA triples.
+// 128 planes: a 2 x 32 tile (one run pair, GW = 4 column groups); 64 planes: 4 x 32 (two run
+// pairs, GW = 2).  y2 stays in LDS as MFMA A fragments ([run][k-step][hi, lo][64 lanes] x 16 B,
+// 32 KB) read per k-step.  Chunk c = conv3 column tiles GW c .. GW c + GW - 1 (wave (pair, g):
+// tile GW c + g) = the next conv1's k-steps 2 GW c .. 2 GW c + 2 GW - 1; its LDS buffer holds
+// those channels for every run.  Issue order keeps HBM latency off the critical path: chunk c +
+// 1's residual (and bias) goes out right behind chunk c's last W1 fetch (chunk 0's at the start
+// of conv2's last W2 ring group, conv2's bias with the patch), so the first wait covering it
+// comes RD3 + RD1 k-steps later (bottleneck_tail_kernel issues the residual at the chunk start
+// and waits on it 2 k-steps later, and its epilogue's bias load drains every prefetch).  RD3 /
+// RD1: W3 / W1 ring depths.  (Holding the outputs in registers to store them later as well
+// spilled; an in-place variant through the accumulators was miscompiled: one element stored 16
+// times.)
+
+// dynamic LDS of tail2_kernel: the patch image, later y2 fragments + the chunk buffer
+template <int C>
+constexpr int tail2_lds() {
+  constexpr int FB = C == 128 ? 2 : 4, GW = 4 / (FB / 2);
+  constexpr int cbp = FB * 32 * GW * 64, need = FB * (C / 16) * 2048 + cbp + 64 + cbp;
+  return Img<C, FB, 32, C == 128 ? 2 : 1>::LDS > need ? Img<C, FB, 32, C == 128 ? 2 : 1>::LDS : need;
+}
+
+template <int C, int P1, int RD3, int RD1>
+__global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs p) {
+  constexpr int FB = C == 128 ? 2 : 4, TB = 32;
+  using G = Img<C, FB, TB, C == 128 ? 2 : 1>;  // patch image; NT = 256 threads either way
+  constexpr int PT = G::PT, CT = G::CT, KS = G::KS;
+  constexpr int NR = FB, GW = 4 / (NR / 2);      // runs; column groups per run pair
+  constexpr int C4 = 4 * C, NT3 = C4 / 32, KS3 = C / 16, NT1 = C / 32;
+  constexpr int NCHK = NT3 / GW, KB = 2 * GW;    // chunks of GW tiles; conv1 k-steps per chunk
+  constexpr int Y2B = NR * KS3 * 2048;           // y2 fragments of every run
+  constexpr int CBR = GW * 64, CBP = NR * 32 * CBR;  // chunk buffer: NR x 32 rows x GW x 32 bf16 per plane
+  constexpr int CBLO = CBP + 64;                 // lo plane 64 B off: paired hi / lo stores, distinct banks
+  static_assert(G::NT == 256 && CT == GW && NT1 == GW && KS % P1 == 0 && P1 % 2 == 0, "tail2: wave layout");
+  static_assert(KS3 % RD3 == 0 && RD1 >= 1 && RD1 + 1 <= KB, "tail2: ring depths");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* xhi = smem;
+  unsigned char* xlo = smem + G::PLANE;
+  unsigned char* y2s = smem;
+  unsigned char* cbhi = smem + Y2B;
+  unsigned char* cblo = cbhi + CBLO;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int pp = w / GW, g = w - pp * GW;  // run pair (runs 2 pp, 2 pp + 1), column group
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+  const int ntf = (p.F + FB - 1) / FB, ntt = (p.T + TB - 1) / TB;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = id / (ntf * ntt);
+  const int rem = id - b * (ntf * ntt);
+  const int tf = rem / ntt;
+  const int f0 = tf * FB, t0 = (rem - tf * ntt) * TB;
+  const size_t plane = (size_t)p.F * p.T;
+  // conv2 bias of this lane's y2 registers, fetched before the patch (waited on with it, not
+  // in the y2 conversion, where the wait would also cover chunk 0's residual)
+  float b2v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) b2v[r] = p.b2[32 * g + (r & 3) + 8 * (r >> 2) + 4 * h];
+  stage_patch<G>(make_rsrc(p.y1 + (size_t)b * plane * C), p.F, p.T, f0, t0, tid, xhi, xlo);
+
+  // residual of chunk c, this wave's runs (run 2 pp + i = frequency row f0 + 2 pp + i) and tile
+  const size_t obase = (size_t)b * plane * C4;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out + obase);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res + obase);
+  const int tw = t0 + 4 * h;  // time of register 0
+  const int fw = f0 + 2 * pp;  // frequency row of the wave's first run
+  auto roff = [&](int i, int col, int r) {
+    const int t = tw + (r & 3) + 8 * (r >> 2);
+    return fw + i < p.F && t < p.T ? (((fw + i) * p.T + t) * C4 + col) * 4 : kOOB;
+  };
+  float rv[2][16], b3v;
+  const __amdgpu_buffer_rsrc_t rb3 = make_rsrc(p.b3);
+  auto rload = [&](int c, bool live) {  // !live: the same loads, out of range (branch-free count)
+    const int col = (GW * c + g) * 32 + r32;
+    b3v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb3, live ? col * 4 : kOOB, 0, 0));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        rv[i][r] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rr, live ? roff(i, col, r) : kOOB, 0, 0));
+  };
+
+  // ---- phase 1: conv2 for the wave's two runs, channel tile g; transposed accumulators
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w2);
+  auto wload = [&](int kg, bf16x8& bh, bf16x8& bl) {
+    const int o = ((kg * 2 * CT + g) * 64 + lane) * 16;
+    bh = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, o, 0, 0));
+    bl = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, o + CT * 1024, 0, 0));
+  };
+  auto read_b = [&](int kg, bf16x8 (&xh)[2], bf16x8 (&xl)[2]) {
+    const int tap = kg / G::KC, cb = kg - tap * G::KC;
+    const int kf = tap / 3, kt = tap - kf * 3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int a = G::addr((2 * pp + i) * PT + r32 + kf * PT + kt, 2 * cb + h);
+      xh[i] = *reinterpret_cast<const bf16x8*>(xhi + a);
+      xl[i] = *reinterpret_cast<const bf16x8*>(xlo + a);
+    }
+  };
+  f32x16 acc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  auto mma_t = [&](const bf16x8 (&xh)[2], const bf16x8 (&xl)[2], const bf16x8& bh, const bf16x8& bl) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, xl[i], acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl, xh[i], acc[i], 0, 0, 0);
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, xh[i], acc[i], 0, 0, 0);
+    }
+  };
+  {
+    bf16x8 wh[P1], wl[P1], xh[2][2], xl[2][2];
+#pragma unroll
+    for (int d = 0; d < P1; ++d) wload(d, wh[d], wl[d]);
+    __syncthreads();  // image complete
+    read_b(0, xh[0], xl[0]);
+#pragma unroll 1
+    for (int kg = 0; kg < KS - P1; kg += P1) {
+#pragma unroll
+      for (int u = 0; u < P1; ++u) {
+        read_b(kg + u + 1, xh[(u + 1) & 1], xl[(u + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_t(xh[u & 1], xl[u & 1], wh[u], wl[u]);
+        wload(kg + u + P1, wh[u], wl[u]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // last ring group: no reloads; chunk 0's residual goes out in their place
+    rload(0, true);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < P1; ++u) {
+      if (u + 1 < P1) read_b(KS - P1 + u + 1, xh[(u + 1) & 1], xl[(u + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_t(xh[u & 1], xl[u & 1], wh[u], wl[u]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // ---- phase 2 weights: W3 B fragments [ks][hi, lo][NT3][64][8] (pack_frag_acc k order),
+  // W1' [ks][hi, lo][NT1][64][8]
+  const __amdgpu_buffer_rsrc_t rw3 = make_rsrc(p.w3);
+  const __amdgpu_buffer_rsrc_t rw1 = make_rsrc(p.w1n);
+  auto w3load = [&](int c, int ks, bf16x8& bh, bf16x8& bl) {  // c == NCHK: past the end (zeros)
+    const int o = ((ks * 2 * NT3 + GW * c + g) * 64 + lane) * 16;
+    bh = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3, c < NCHK ? o : kOOB, 0, 0));
+    bl = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3, c < NCHK ? o + NT3 * 1024 : kOOB, 0, 0));
+  };
+  auto w1load = [&](int ks, bf16x8& bh, bf16x8& bl) {
+    const int o = ((ks * 2 * NT1 + g) * 64 + lane) * 16;
+    bh = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1, o, 0, 0));
+    bl = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1, o + NT1 * 1024, 0, 0));
+  };
+  // W3 / W1 rings (slot j = k-step j mod RD3 / RD1); chunk 0's first RD3 W3 k-steps go out
+  // before the y2 conversion
+  bf16x8 ch_[RD3], cl_[RD3], uh_[RD1], ul_[RD1];
+#pragma unroll
+  for (int j = 0; j < RD3; ++j) w3load(0, j, ch_[j], cl_[j]);
+
+  // ---- y2 = relu(acc + b2) -> LDS fragments [run][k-step][hi, lo][lane] (k-step 2 g + s2 =
+  // registers 8 s2 .. 8 s2 + 7 of channel tile g)
+  __syncthreads();  // every wave is done reading the image
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 vh, vl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int r = 8 * s2 + e;
+        const float y = fmaxf(acc[i][r] + b2v[r], 0.f);
+        const __bf16 hh = (__bf16)y;
+        vh[e] = hh;
+        vl[e] = (__bf16)(y - (float)hh);
+      }
+      const int o = (((2 * pp + i) * KS3 + 2 * g + s2) * 2) * 1024 + lane * 16;
+      *reinterpret_cast<bf16x8*>(y2s + o) = vh;
+      *reinterpret_cast<bf16x8*>(y2s + o + 1024) = vl;
+    }
+  __syncthreads();
+
+  auto read_y2 = [&](int ks, bf16x8 (&ah)[2], bf16x8 (&al)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int o = (((2 * pp + i) * KS3 + ks) * 2) * 1024 + lane * 16;
+      ah[i] = *reinterpret_cast<const bf16x8*>(y2s + o);
+      al[i] = *reinterpret_cast<const bf16x8*>(y2s + o + 1024);
+    }
+  };
+  // 16-B chunks XOR-swizzled by row as Img's (256-B rows: row & 15; 128-B rows: (row >> 1) & 7)
+  auto cbaddr = [](int row, int c16) { return row * CBR + ((c16 ^ (CBR == 256 ? row & 15 : (row >> 1) & 7)) << 4); };
+  auto read_cb = [&](int kk, bf16x8 (&ah)[2], bf16x8 (&al)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int a = cbaddr((2 * pp + i) * 32 + r32, 2 * kk + h);
+      ah[i] = *reinterpret_cast<const bf16x8*>(cbhi + a);
+      al[i] = *reinterpret_cast<const bf16x8*>(cblo + a);
+    }
+  };
+  auto mma2 = [](f32x16 (&d)[2], const bf16x8 (&ah)[2], const bf16x8 (&al)[2], const bf16x8& bh,
+                 const bf16x8& bl) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      d[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, d[i], 0, 0, 0);
+      d[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, d[i], 0, 0, 0);
+      d[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, d[i], 0, 0, 0);
+    }
+  };
+
+  f32x16 acc1[2], a3[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc1[i][r] = 0.f;
+#pragma unroll 1
+  for (int c = 0; c < NCHK; ++c) {
+#pragma unroll
+    for (int j = 0; j < RD1; ++j) w1load(KB * c + j, uh_[j], ul_[j]);  // land during the chunk's conv3
+    // conv3, column tile GW c + g, the wave's two runs
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a3[i][r] = 0.f;
+    bf16x8 ah[2][2], al[2][2];
+    read_y2(0, ah[0], al[0]);
+#pragma unroll
+    for (int q = 0; q < KS3; ++q) {
+      if (q + 1 < KS3) read_y2(q + 1, ah[(q + 1) & 1], al[(q + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma2(a3, ah[q & 1], al[q & 1], ch_[q % RD3], cl_[q % RD3]);
+      if (q + RD3 < KS3) w3load(c, q + RD3, ch_[q % RD3], cl_[q % RD3]);
+      else w3load(c + 1, q + RD3 - KS3, ch_[q % RD3], cl_[q % RD3]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (c > 0) __syncthreads();  // every wave is done reading chunk c - 1 from the buffer
+    // epilogue: out = relu(a3 + b3 + res) -> HBM and as bf16 hi / lo rows of the chunk buffer.
+    // The first wait covering these stores is the one on the W1 fetch that conv1's k-step 0
+    // issues after them, RD1 k-steps later (stores count in vmcnt like loads)
+    {
+      const int col = (GW * c + g) * 32 + r32;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float y = fmaxf(a3[i][r] + b3v + rv[i][r], 0.f);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, roff(i, col, r), 0, 0);
+          // lanes l, l ^ 1 hold columns c, c ^ 1: the even lane stores both hi halves, the odd
+          // lane both lo halves
+          const __bf16 hh = (__bf16)y;
+          const __bf16 ll = (__bf16)(y - (float)hh);
+          const unsigned short hb = __builtin_bit_cast(unsigned short, hh);
+          const unsigned short lb = __builtin_bit_cast(unsigned short, ll);
+          const unsigned send = (lane & 1) ? hb : lb;
+          const unsigned recv = (unsigned)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
+          const int row = (2 * pp + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int cc = g * 32 + (r32 & ~1);
+          const int a = cbaddr(row, cc >> 3) + (cc & 7) * 2;
+          if (lane & 1)
+            *reinterpret_cast<unsigned*>(cblo + a) = recv | ((unsigned)lb << 16);
+          else
+            *reinterpret_cast<unsigned*>(cbhi + a) = (unsigned)hb | (recv << 16);
+        }
+      }
+    }
+    __syncthreads();  // the chunk's GW x 32 channels of every run are in LDS
+    // next conv1: k-steps KB c .. KB c + KB - 1, output tile g, the wave's two runs
+    read_cb(0, ah[0], al[0]);
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      if (kk + 1 < KB) read_cb(kk + 1, ah[(kk + 1) & 1], al[(kk + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma2(acc1, ah[kk & 1], al[kk & 1], uh_[kk % RD1], ul_[kk % RD1]);
+      if (kk + RD1 < KB) w1load(KB * c + kk + RD1, uh_[kk % RD1], ul_[kk % RD1]);
+      if (kk + RD1 + 1 == KB) rload(c + 1, c + 1 < NCHK);  // right behind the chunk's last W1 fetch
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // y1' = relu(acc1 + b1') -> y1n [B][F][T][C], output tile g
+  {
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc(p.y1n + (size_t)b * plane * C);
+    const int col = g * 32 + r32;
+    const float bv = p.b1n[col];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int t = tw + (r & 3) + 8 * (r >> 2);
+        const float y = fmaxf(acc1[i][r] + bv, 0.f);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ry,
+                                              fw + i < p.F && t < p.T ? (((fw + i) * p.T + t) * C + col) * 4 : kOOB,
+                                              0, 0);
+      }
+  }
+}
+
 template <int C, int FB, int TB, int MINB, int WN = 1>
 void launch_k(const Conv3x3Args& p, hipStream_t s) {
   using G = Img<C, FB, TB, WN>;
@@ -649,6 +953,13 @@ void launch_tail_k(const BottleneckTailArgs& p, hipStream_t s) {
     hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB, NC, false, P1U, PM>), dim3(nblk), dim3(G::NT), G::LDS,
                        s, p);
 }
+
+template <int C, int RD3, int RD1>
+void launch_tail2(const BottleneckTailArgs& p, hipStream_t s) {
+  constexpr int FB = C == 128 ? 2 : 4;
+  const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + 31) / 32);
+  hipLaunchKernelGGL((tail2_kernel<C, 4, RD3, RD1>), dim3(nblk), dim3(256), tail2_lds<C>(), s, p);
+}
 }  // namespace
 
 bool bottleneck_tail_supported(int C) { return C == 32 || C == 64 || C == 128; }
@@ -667,8 +978,12 @@ void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s) {
     launch_tail_k<32, 4, 32, 1, 3, 1>(p, s);  // 128 positions, 4 waves, 26 KB image: 3 blocks / CU
   else if (C == 32)
     launch_tail_k<32, 4, 64, 1, 4, 1>(p, s);  // 256 positions, 8 waves, 50 KB image: 2 blocks / CU
+  else if (C == 64 && p.w1n && p.variant == 3)
+    launch_tail2<64, 4, 2>(p, s);
   else if (C == 64)  // (a 2 x 32 tile: C3 -1.3 %)
     launch_tail_k<64, 4, 32, 1, 3, 2, 1, 2>(p, s);  // 128 positions, 4 waves, 51 KB image: 3 blocks / CU
+  else if (p.w1n && p.variant == 3)
+    launch_tail2<128, 4, 4>(p, s);
   else if (p.w1n)
     // with the next conv1 (per-chunk barriers), two independent blocks per CU: C3 +1.5 % over the
     // 4 x 32 tile (one 102 KB block per CU)
