@@ -137,7 +137,8 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *                  1 for ECAPA-TDNN; segmented ECAPA batches always run as one range
  *   "x3_variant"   bf16x3 conv-GEMM tile family (all with swizzled LDS rows): 3 = 128x128,
  *                  4 = 256x128 (ResNet default), 5 = 256x256 where N % 256 == 0, else 256x128
- *                  (ECAPA-TDNN, SimAM-ResNet and HuBERT default)
+ *                  (SimAM-ResNet and HuBERT default), 6 = 5 with the 256x256 tile on 16x16x32
+ *                  MFMAs (ECAPA-TDNN default)
  *   "res2_fused"   1 = one res2_chain launch per SE_Res2Block (default), 0 = 7 GEMMs
  *   "res2_variant" res2_chain kernel: 128-row windows with halo recompute: 0 = 2 x 2 waves,
  *                  2 = 4 waves on N with 4 W k-steps in flight (C = 128; else as 0), 3 = 8 waves

@@ -55,10 +55,10 @@ def _hip_model(arch, seed, precision=1, variant=5, **kw):
     return m.to(DEV), sd
 
 
-# the shipped bf16x3 tile families (x3_variant 5 = 256x256 ECAPA / HuBERT default, 4 = 256x128
-# ResNet default, 3 = 128x128) and the exact-f32 kernels (precision 0)
-PREC = [(1, 5), (1, 4), (1, 3), (0, 5)]
-PREC_IDS = ["bf16x3_256sq", "bf16x3_256swz", "bf16x3_128swz", "f32"]
+# the shipped bf16x3 tile families (x3_variant 5 = 256x256 ECAPA / HuBERT default, 6 = the same tile
+# on 16x16x32 MFMAs, 4 = 256x128 ResNet default, 3 = 128x128) and the exact-f32 kernels (precision 0)
+PREC = [(1, 5), (1, 6), (1, 4), (1, 3), (0, 5)]
+PREC_IDS = ["bf16x3_256sq", "bf16x3_256mf16", "bf16x3_256swz", "bf16x3_128swz", "f32"]
 
 
 @pytest.mark.parametrize("prec", PREC, ids=PREC_IDS)

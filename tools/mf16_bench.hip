@@ -47,7 +47,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
 template <int MF>
 __device__ __forceinline__ int loff(int row, int byte) {
   const int q = (row >> 2) & 3;
-  const int f = MF == 32 ? q : ((0x1320 >> (4 * q)) & 3);
+  const int f = MF == 32 ? q : ((0x1320 >> (4 * q)) & 3);  // MF 16 / 17 share the layout
   return row * ROWB + ((((byte >> 4) ^ f) & 3) << 4) + (byte & 15);
 }
 
@@ -199,6 +199,36 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(const float* __restrict__ A
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], c, 0, 0, 0);
         }
     };
+    // MF 17: snake order (0,0) (0,1) (1,1) (1,0), each quarter re-reading only the fragments it
+    // does not share with the previous one (32 instead of 48 ds_read_b128 per k-tile)
+    bf16x8 ah[2], al[2], bh[4], bl[4];
+    auto rdA = [&](const unsigned char* st, int ih) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int o = loff<16>(wm * 64 + (ih * 2 + i) * 16 + r16, qk * 16);
+        ah[i] = *reinterpret_cast<const bf16x8*>(st + o);
+        al[i] = *reinterpret_cast<const bf16x8*>(st + IMG + o);
+      }
+    };
+    auto rdB = [&](const unsigned char* st, int jh) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int o = loff<16>(wn * 128 + (jh * 4 + j) * 16 + r16, qk * 16);
+        bh[j] = *reinterpret_cast<const bf16x8*>(st + 2 * IMG + o);
+        bl[j] = *reinterpret_cast<const bf16x8*>(st + 3 * IMG + o);
+      }
+    };
+    auto mm = [&](int ih, int jh) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4& c = acc[ih * 2 + i][jh * 4 + j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], c, 0, 0, 0);
+        }
+    };
     const int nk = K / BK;
     load_tile(0, true);
     store_tile(0);
@@ -206,12 +236,27 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(const float* __restrict__ A
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
-      mma_q(buf, 0, 0);
-      mma_q(buf, 0, 1);
-      store_tile(buf ^ 1);
-      load_tile((kt + 2) * BK, kt + 2 < nk);
-      mma_q(buf, 1, 0);
-      mma_q(buf, 1, 1);
+      if constexpr (MF == 17) {
+        const unsigned char* st = smem + buf * STAGE;
+        rdA(st, 0);
+        rdB(st, 0);
+        mm(0, 0);
+        rdB(st, 1);
+        mm(0, 1);
+        store_tile(buf ^ 1);
+        load_tile((kt + 2) * BK, kt + 2 < nk);
+        rdA(st, 1);
+        mm(1, 1);
+        rdB(st, 0);
+        mm(1, 0);
+      } else {
+        mma_q(buf, 0, 0);
+        mma_q(buf, 0, 1);
+        store_tile(buf ^ 1);
+        load_tile((kt + 2) * BK, kt + 2 < nk);
+        mma_q(buf, 1, 0);
+        mma_q(buf, 1, 1);
+      }
       __syncthreads();
     }
 #pragma unroll
@@ -273,13 +318,16 @@ int main(int argc, char** argv) {
     if (mf == 32)
       hipLaunchKernelGGL(gemm_kernel<32>, dim3(nwg), dim3(NT), 2 * STAGE, s, da, (const __bf16*)dh,
                          (const __bf16*)dl, o, M, N, K);
+    else if (mf == 17)
+      hipLaunchKernelGGL(gemm_kernel<17>, dim3(nwg), dim3(NT), 2 * STAGE, s, da, (const __bf16*)dh,
+                         (const __bf16*)dl, o, M, N, K);
     else
       hipLaunchKernelGGL(gemm_kernel<16>, dim3(nwg), dim3(NT), 2 * STAGE, s, da, (const __bf16*)dh,
                          (const __bf16*)dl, o, M, N, K);
   };
   // interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24)
   for (int round = 0; round < 4; ++round) {
-    for (int mf : {32, 16}) {
+    for (int mf : {32, 16, 17}) {
       float* o = mf == 32 ? o1 : o2;
       run(mf, o);
       CK(hipStreamSynchronize(s));

@@ -12,7 +12,13 @@
 #include <random>
 #include <vector>
 
-#include "../wespeaker_hubert_amd/csrc/conv3x3_img.h"
+// the kernels are compiled into this tool (not linked from libwsp_hip.so) with phase stamps on
+__device__ unsigned long long* g_stamps;
+#define WSP_TAIL_STAMP(k)                                                           \
+  do {                                                                              \
+    if (threadIdx.x == 0) g_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#include "../wespeaker_hubert_amd/csrc/conv3x3_img.hip"
 
 using namespace wsp;
 
@@ -73,6 +79,12 @@ int main(int argc, char** argv) {
     CK(hipMemset(out[i], 0xFF, npos * 4 * C * 4));
     CK(hipMemset(y1n[i], 0xFF, npos * C * 4));
   }
+  const int FBk = C == 128 ? 2 : C == 64 ? 4 : 8;
+  const int nblk = B * ((F + FBk - 1) / FBk) * ((T + 31) / 32);
+  unsigned long long* dst;
+  CK(hipMalloc(&dst, (size_t)nblk * 16 * 8));
+  CK(hipMemset(dst, 0, (size_t)nblk * 16 * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dst, sizeof(dst)));
   const int vars[2] = {1, 3};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -116,6 +128,29 @@ int main(int argc, char** argv) {
     }
     std::printf("\n");
   };
+  {  // phase durations of tail2_kernel (last launch), cycles averaged over blocks
+    std::vector<unsigned long long> st((size_t)nblk * 16);
+    CK(hipMemcpy(st.data(), dst, st.size() * 8, hipMemcpyDeviceToHost));
+    const int ks[7] = {0, 1, 2, 3, 4, 5, 6};
+    const char* nm[8] = {"patch", "phase1", "y2", "chunk0", "chunk1", "chunk2", "chunk3+", "tail"};
+    double sum[8] = {0};
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int b = 0; b < nblk; ++b) {
+      const unsigned long long* q = &st[(size_t)b * 16];
+      for (int i = 0; i < 6; ++i) sum[i] += (double)(q[ks[i] + 1] - q[ks[i]]);
+      sum[6] += (double)(q[7] - q[6]);
+      sum[7] += (double)(q[15] - q[7]);
+      t0 = std::min(t0, q[0]);
+      t1 = std::max(t1, q[15]);
+    }
+    std::printf("tail2 phases (cycles/block):");
+    double tot = 0;
+    for (int i = 0; i < 8; ++i) {
+      std::printf(" %s %.0f", nm[i], sum[i] / nblk);
+      tot += sum[i] / nblk;
+    }
+    std::printf(" | block %.0f, span %llu cycles, %d blocks\n", tot, t1 - t0, nblk);
+  }
   cmp("out", out, npos * 4 * C, 4 * C);
   cmp("y1n", y1n, npos * C, C);
   return 0;

@@ -23,6 +23,12 @@
 #include "conv3x3_img.h"
 #include "gemm_common.h"
 
+// Development stamps: tools/tail_check.cpp defines WSP_TAIL_STAMP(k) to record s_memtime at
+// tail2_kernel's phase boundaries; in the library it expands to nothing.
+#ifndef WSP_TAIL_STAMP
+#define WSP_TAIL_STAMP(k)
+#endif
+
 namespace wsp {
 
 namespace {
@@ -30,14 +36,15 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-template <int C, int FB, int TB, int WN = 1>
+template <int C, int FB, int TB, int WN = 1, int NWO = 0>
 struct Img {
   static constexpr int PT = TB + 2;
   static constexpr int IR = (FB + 2) * PT;  // patch positions
   static constexpr int RB = 2 * C;          // bytes per image row and plane
   static constexpr int PLANE = IR * RB;
   static constexpr int LDS = 2 * PLANE;
-  static constexpr int NW = FB * TB / 32 * WN;  // waves: 32 positions (one time run) x C / WN channels each
+  // waves: 32 positions (one time run) x C / WN channels each (NWO: a kernel's own wave count)
+  static constexpr int NW = NWO ? NWO : FB * TB / 32 * WN;
   static constexpr int NT = NW * 64;
   static constexpr int CT = C / 32;         // 32-channel column tiles
   static constexpr int TN = CT / WN;        // column tiles per wave
@@ -623,15 +630,15 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
 // dynamic LDS of tail2_kernel: the patch image, later y2 fragments + the chunk buffer
 template <int C>
 constexpr int tail2_lds() {
-  constexpr int FB = C == 128 ? 2 : 4, GW = 4 / (FB / 2);
+  constexpr int FB = C == 128 ? 2 : C == 64 ? 4 : 8, GW = 4 / (FB / 2);
   constexpr int cbp = FB * 32 * GW * 64, need = FB * (C / 16) * 2048 + cbp + 64 + cbp;
-  return Img<C, FB, 32, C == 128 ? 2 : 1>::LDS > need ? Img<C, FB, 32, C == 128 ? 2 : 1>::LDS : need;
+  return Img<C, FB, 32>::LDS > need ? Img<C, FB, 32>::LDS : need;
 }
 
 template <int C, int P1, int RD3, int RD1>
 __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs p) {
-  constexpr int FB = C == 128 ? 2 : 4, TB = 32;
-  using G = Img<C, FB, TB, C == 128 ? 2 : 1>;  // patch image; NT = 256 threads either way
+  constexpr int FB = C == 128 ? 2 : C == 64 ? 4 : 8, TB = 32;
+  using G = Img<C, FB, TB, 1, 4>;  // patch image staged by the 4 waves
   constexpr int PT = G::PT, CT = G::CT, KS = G::KS;
   constexpr int NR = FB, GW = 4 / (NR / 2);      // runs; column groups per run pair
   constexpr int C4 = 4 * C, NT3 = C4 / 32, KS3 = C / 16, NT1 = C / 32;
@@ -661,6 +668,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
   const int tf = rem / ntt;
   const int f0 = tf * FB, t0 = (rem - tf * ntt) * TB;
   const size_t plane = (size_t)p.F * p.T;
+  WSP_TAIL_STAMP(0);
   // conv2 bias of this lane's y2 registers, fetched before the patch (waited on with it, not
   // in the y2 conversion, where the wait would also cover chunk 0's residual)
   float b2v[16];
@@ -726,6 +734,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
 #pragma unroll
     for (int d = 0; d < P1; ++d) wload(d, wh[d], wl[d]);
     __syncthreads();  // image complete
+    WSP_TAIL_STAMP(1);
     read_b(0, xh[0], xl[0]);
 #pragma unroll 1
     for (int kg = 0; kg < KS - P1; kg += P1) {
@@ -750,6 +759,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
     }
   }
 
+  WSP_TAIL_STAMP(2);
   // ---- phase 2 weights: W3 B fragments [ks][hi, lo][NT3][64][8] (pack_frag_acc k order),
   // W1' [ks][hi, lo][NT1][64][8]
   const __amdgpu_buffer_rsrc_t rw3 = make_rsrc(p.w3);
@@ -791,6 +801,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
       *reinterpret_cast<bf16x8*>(y2s + o + 1024) = vl;
     }
   __syncthreads();
+  WSP_TAIL_STAMP(3);
 
   auto read_y2 = [&](int ks, bf16x8 (&ah)[2], bf16x8 (&al)[2]) {
 #pragma unroll
@@ -800,8 +811,11 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
       al[i] = *reinterpret_cast<const bf16x8*>(y2s + o + 1024);
     }
   };
-  // 16-B chunks XOR-swizzled by row as Img's (256-B rows: row & 15; 128-B rows: (row >> 1) & 7)
-  auto cbaddr = [](int row, int c16) { return row * CBR + ((c16 ^ (CBR == 256 ? row & 15 : (row >> 1) & 7)) << 4); };
+  // 16-B chunks XOR-swizzled by row as Img's (256-B rows: row & 15; 128-B: (row >> 1) & 7; 64-B:
+  // (row >> 2) & 3)
+  auto cbaddr = [](int row, int c16) {
+    return row * CBR + ((c16 ^ (CBR == 256 ? row & 15 : CBR == 128 ? (row >> 1) & 7 : (row >> 2) & 3)) << 4);
+  };
   auto read_cb = [&](int kk, bf16x8 (&ah)[2], bf16x8 (&al)[2]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -887,6 +901,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
       if (kk + RD1 + 1 == KB) rload(c + 1, c + 1 < NCHK);  // right behind the chunk's last W1 fetch
       __builtin_amdgcn_sched_barrier(0);
     }
+    WSP_TAIL_STAMP(4 + c);
   }
   // y1' = relu(acc1 + b1') -> y1n [B][F][T][C], output tile g
   {
@@ -904,6 +919,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
                                               0, 0);
       }
   }
+  WSP_TAIL_STAMP(15);
 }
 
 template <int C, int FB, int TB, int MINB, int WN = 1>
@@ -954,11 +970,11 @@ void launch_tail_k(const BottleneckTailArgs& p, hipStream_t s) {
                        s, p);
 }
 
-template <int C, int RD3, int RD1>
+template <int C, int P1, int RD3, int RD1>
 void launch_tail2(const BottleneckTailArgs& p, hipStream_t s) {
-  constexpr int FB = C == 128 ? 2 : 4;
+  constexpr int FB = C == 128 ? 2 : C == 64 ? 4 : 8;
   const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + 31) / 32);
-  hipLaunchKernelGGL((tail2_kernel<C, 4, RD3, RD1>), dim3(nblk), dim3(256), tail2_lds<C>(), s, p);
+  hipLaunchKernelGGL((tail2_kernel<C, P1, RD3, RD1>), dim3(nblk), dim3(256), tail2_lds<C>(), s, p);
 }
 }  // namespace
 
@@ -974,16 +990,18 @@ void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s) {
   WSP_CHECK(!p.w1n || (p.b1n && p.y1n && p.y1n != p.out && p.y1n != p.y1 && p.y1n != p.res),
             "bottleneck_tail: next conv1 needs bias and a separate output");
   // <C, FB, TB, WN, MINB, NC[, NC and MINB with the next conv1]>
-  if (C == 32 && p.w1n)
+  if (C == 32 && p.w1n && p.variant == 3)
+    launch_tail2<32, 2, 2, 1>(p, s);  // 256 positions (8 runs), 4 waves, 64 KB: 2 blocks / CU
+  else if (C == 32 && p.w1n)
     launch_tail_k<32, 4, 32, 1, 3, 1>(p, s);  // 128 positions, 4 waves, 26 KB image: 3 blocks / CU
   else if (C == 32)
     launch_tail_k<32, 4, 64, 1, 4, 1>(p, s);  // 256 positions, 8 waves, 50 KB image: 2 blocks / CU
   else if (C == 64 && p.w1n && p.variant == 3)
-    launch_tail2<64, 4, 2>(p, s);
+    launch_tail2<64, 4, 4, 2>(p, s);
   else if (C == 64)  // (a 2 x 32 tile: C3 -1.3 %)
     launch_tail_k<64, 4, 32, 1, 3, 2, 1, 2>(p, s);  // 128 positions, 4 waves, 51 KB image: 3 blocks / CU
   else if (p.w1n && p.variant == 3)
-    launch_tail2<128, 4, 4>(p, s);
+    launch_tail2<128, 4, 4, 4>(p, s);
   else if (p.w1n)
     // with the next conv1 (per-chunk barriers), two independent blocks per CU: C3 +1.5 % over the
     // 4 x 32 tile (one 102 KB block per CU)

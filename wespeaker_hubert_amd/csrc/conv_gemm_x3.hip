@@ -62,7 +62,7 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
               "conv_gemm_x3: column sums need a uniform batch with T >= block rows and no row bias");
   }
   WSP_CHECK(p.Kp % 64 == 0, "conv_gemm_x3: packed K must be a multiple of 64");
-  WSP_CHECK(variant == 3 || variant == 4 || variant == 5, "conv_gemm_x3: tile family must be 3, 4 or 5");
+  WSP_CHECK(variant >= 3 && variant <= 6, "conv_gemm_x3: tile family must be 3, 4, 5 or 6");
   const __bf16* h = static_cast<const __bf16*>(whi);
   const __bf16* l = static_cast<const __bf16*>(wlo);
   x3::TileFn f;
@@ -82,7 +82,10 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
     // variant 5: 256 x 256 (8 waves 4 x 2, 64 x 128 per wave) wherever N allows it: in-model
     // C x C -10 %, conv_cat -15 %, HuBERT fc1 -18 %, fc2 -20 %, CNN -12 % vs 256 x 128 (with
     // the per-tile residual epilogue and the A&S GELU; the libm erff made fc1's epilogue lose).
-    f = x3::t_4x2_2x4_sw1;
+    // variant 6: the same tile on v_mfma_f32_16x16x32_bf16 (MI355X holds a higher clock on that
+    // shape; ECAPA default, C2 +0.8-1.2 %; HuBERT measured neutral: fc2 / CNN faster, QKV /
+    // out_proj slower)
+    f = variant == 6 ? x3::t_4x2_2x4_mf16 : x3::t_4x2_2x4_sw1;
   } else {
     f = x3::t_4x2_2x2_sw;  // variant 5 with N % 256 != 0
   }

@@ -21,22 +21,29 @@ constexpr int BK = 32;
 // unpadded 64-B rows with the 16-B chunk XOR-swizzled by (row >> 2) & 3 —
 // both conflict-free for the fragment reads (row = lane & 31, chunk = 2s + h);
 // the swizzled form is 20 % smaller (two 128 x 128 blocks fit a CU).
-template <bool SWZ>
+// MF = 16 (v_mfma_f32_16x16x32_bf16 fragments: row = lane & 15, chunk = lane >> 4) swizzles
+// by the {0, 2, 3, 1} map of (row >> 2) & 3, which keeps each ds_read_b128 lane group on 16
+// distinct 16-B slots of the bank row (tools/mf16_bench.hip).
+template <bool SWZ, int MF = 32>
 struct Lds {
   static constexpr int ROWB = SWZ ? 64 : 80;
   static constexpr int SKEW = SWZ ? 0 : 64;  // lo W image offset (padded rows: 16-bank skew)
   __device__ __forceinline__ static int off(int row, int byte) {
-    if constexpr (SWZ) return row * 64 + ((((byte >> 4) ^ (row >> 2)) & 3) << 4) + (byte & 15);
+    static_assert(MF == 32 || SWZ, "16x16 fragments need the swizzled rows");
+    if constexpr (SWZ && MF == 16)
+      return row * 64 + ((((byte >> 4) ^ (0x1320 >> (4 * ((row >> 2) & 3)))) & 3) << 4) + (byte & 15);
+    else if constexpr (SWZ) return row * 64 + ((((byte >> 4) ^ (row >> 2)) & 3) << 4) + (byte & 15);
     else return row * 80 + byte;
   }
 };
 
 template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D = false, bool SWZ = false,
-          int NSET = 2>
+          int NSET = 2, int MF = 32>
 __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArgs p,
                                                                const __bf16* __restrict__ whi,
                                                                const __bf16* __restrict__ wlo) {
-  using L = Lds<SWZ>;
+  using L = Lds<SWZ, MF>;
+  static_assert(MF == 32 || NSET == 1, "16x16 MFMA: one-staging-set wide tiles only");
   constexpr int ROWB = L::ROWB;
   constexpr int NT = WM * WN * 64;
   constexpr int BM = WM * TM * 32;
@@ -163,7 +170,68 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   };
 
   const int nk = p.Kp / BK;
-  if constexpr (NSET == 1) {
+  if constexpr (MF == 16) {
+    // 16x16x32: one MFMA spans the whole 32-deep k-tile.  The wave tile is 2 TM x 2 TN blocks
+    // of 16 x 16; sub-step s of a k-tile runs the quarters (ih, jh) = (0, 0), (0, 1) (s = 0)
+    // and (1, 1), (1, 0) (s = 1) — a snake, so each quarter re-reads only the fragments it does
+    // not share with the previous one and 6 TM + 6 TN... fragment registers stay live
+    const int r16 = lane & 15, qk = lane >> 4;
+    f32x4 acc16[2 * TM][2 * TN];
+#pragma unroll
+    for (int i = 0; i < 2 * TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2 * TN; ++j) acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 fah[TM], fal[TM], fbh[TN], fbl[TN];
+    auto rdA = [&](const unsigned char* st, int ih) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int o = L::off(wm * TM * 32 + (ih * TM + i) * 16 + r16, qk * 16);
+        fah[i] = *reinterpret_cast<const bf16x8*>(st + o);
+        fal[i] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + o);
+      }
+    };
+    auto rdB = [&](const unsigned char* st, int jh) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int o = L::off(wn * TN * 32 + (jh * TN + j) * 16 + r16, qk * 16);
+        fbh[j] = *reinterpret_cast<const bf16x8*>(st + 2 * A_BYTES + o);
+        fbl[j] = *reinterpret_cast<const bf16x8*>(st + 2 * A_BYTES + B_LO + o);
+      }
+    };
+    auto mm = [&](int ih, int jh) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          f32x4& c = acc16[ih * TM + i][jh * TN + j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fal[i], fbh[j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fah[i], fbl[j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fah[i], fbh[j], c, 0, 0, 0);
+        }
+    };
+    load_tile(ra0, rb0, 0, true);
+    store_tile(ra0, rb0, 0);
+    load_tile(ra0, rb0, BK, true);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      const unsigned char* st = smem + buf * STAGE;
+      rdA(st, 0);
+      rdB(st, 0);
+      mm(0, 0);
+      rdB(st, 1);
+      mm(0, 1);
+      store_tile(ra0, rb0, buf ^ 1);  // past-the-end tiles are zeros nobody reads
+      load_tile(ra0, rb0, (kt + 2) * BK, kt + 2 < nk);
+      rdA(st, 1);
+      mm(1, 1);
+      rdB(st, 0);
+      mm(1, 0);
+      __syncthreads();
+    }
+    gemm_epilogue16<2 * TM, 2 * TN, WM, WN>(p, acc16, m0, n0, wm, wn, lane, smem);
+    return;
+  } else if constexpr (NSET == 1) {
     // One register set (wide wave tiles: the accumulators leave no room for a
     // second): tile k+1, loaded during step k-1, is written to the free buffer
     // between step k's two sub-steps, and tile k+2 is issued right after it.
@@ -237,33 +305,33 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void conv_gemm_x3(const ConvGemmArg
   gemm_epilogue<TM, TN, WM, WN>(p, acc, m0, n0, wm, wn, lane, smem);
 }
 
-template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D, bool SWZ, int NSET>
+template <int WM, int WN, int TM, int TN, int AMODE, bool UNI, int ROLE, bool C2D, bool SWZ, int NSET, int MF = 32>
 void launch_x3_k(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = WM * WN * 64;
   constexpr int ROWB = Lds<SWZ>::ROWB;
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
   const size_t lds = (size_t)2 * (2 * BM * ROWB + 2 * BN * ROWB + Lds<SWZ>::SKEW);
-  hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, AMODE, UNI, ROLE, C2D, SWZ, NSET>), dim3(nwg), dim3(NT), lds, s,
-                     p, whi, wlo);
+  hipLaunchKernelGGL((conv_gemm_x3<WM, WN, TM, TN, AMODE, UNI, ROLE, C2D, SWZ, NSET, MF>), dim3(nwg), dim3(NT), lds,
+                     s, p, whi, wlo);
   WSP_HIP(hipGetLastError());
 }
 
-template <int WM, int WN, int TM, int TN, bool SWZ = false, int NSET = 2>
+template <int WM, int WN, int TM, int TN, bool SWZ = false, int NSET = 2, int MF = 32>
 void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
   if (p.conv2d) {
-    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, true, SWZ, NSET>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, true, SWZ, NSET, MF>(p, whi, wlo, s);
     return;
   }
   const bool uni = uniform_ktiles(p);
   if (p.amode == kAAdd) {
     if (uni)
-      launch_x3_k<WM, WN, TM, TN, kAAdd, true, 0, false, SWZ, NSET>(p, whi, wlo, s);
+      launch_x3_k<WM, WN, TM, TN, kAAdd, true, 0, false, SWZ, NSET, MF>(p, whi, wlo, s);
     else
-      launch_x3_k<WM, WN, TM, TN, kAAdd, false, 0, false, SWZ, NSET>(p, whi, wlo, s);
+      launch_x3_k<WM, WN, TM, TN, kAAdd, false, 0, false, SWZ, NSET, MF>(p, whi, wlo, s);
   } else if (!uni) {
-    launch_x3_k<WM, WN, TM, TN, kACat, false, 0, false, SWZ, NSET>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, false, 0, false, SWZ, NSET, MF>(p, whi, wlo, s);
   } else if (p.role == 1) {
-    launch_x3_k<WM, WN, TM, TN, kACat, true, 1, false, SWZ, NSET>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 1, false, SWZ, NSET, MF>(p, whi, wlo, s);
   } else if constexpr (NSET == 2 && TM * TN <= 4) {
     // residual convs: the residual is loaded ahead of the last two k-tiles (ROLE 2)
     if (p.res && p.role == 2)
@@ -271,7 +339,7 @@ void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo,
     else
       launch_x3_k<WM, WN, TM, TN, kACat, true, 0, false, SWZ, NSET>(p, whi, wlo, s);
   } else {
-    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, false, SWZ, NSET>(p, whi, wlo, s);
+    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, false, SWZ, NSET, MF>(p, whi, wlo, s);
   }
 }
 
@@ -285,6 +353,7 @@ void t_8x1_1x2_sw(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t
 void t_2x2_2x2_sw(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);   // 128 x 128 swizzled (v3)
 void t_4x2_2x2_sw(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);   // 256 x 128 swizzled (v4)
 void t_4x2_2x4_sw1(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);  // 256 x 256, one set (v5)
+void t_4x2_2x4_mf16(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);  // v5 on 16x16x32 (v6)
 }  // namespace x3
 
 }  // namespace wsp

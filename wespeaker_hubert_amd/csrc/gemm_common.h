@@ -415,6 +415,144 @@ __device__ __forceinline__ void gemm_epilogue_res_pre(const ConvGemmArgs& p, f32
   }
 }
 
+// The same epilogue for 16x16 accumulator tiles (v_mfma_f32_16x16x32_bf16 C/D map: col =
+// lane & 15, row = 4 (lane >> 4) + r, r = 0..3): a wave's TM x TN tiles of 16 x 16.  The
+// residual is read per tile (4 loads) right where it is added.
+template <int TM, int TN, int ACT, bool RB, bool CS = false, bool RES = false>
+__device__ __forceinline__ void gemm_epilogue_store16(const ConvGemmArgs& p, f32x4 (&acc)[TM][TN], int m0, int n0,
+                                                      int wm, int wn, int lane, double (*cs)[2] = nullptr) {
+  const int c16 = lane & 15;
+  const int q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
+  const int ldo4 = p.ldo * 4;
+  const __amdgpu_buffer_rsrc_t rres = make_rsrc(RES ? p.res : p.out);
+  const int ldr4 = p.ldres * 4;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + (wn * TN + j) * 16 + c16;
+    const float bv = p.bias ? p.bias[col] : 0.f;
+    const float sc = p.scale ? p.scale[col] : 1.f;
+    const float sh = p.scale ? p.shift[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int t0 = m0 + (wm * TM + i) * 16;  // the tile's first row
+      const int row0 = t0 + 4 * q;
+      const int lim = p.M - row0;  // rows row0 + r with r < lim exist
+      const int base = row0 * ldo4 + col * 4;
+      int mode = 2;  // CS: as gemm_epilogue_store, per 16-row tile
+      if constexpr (CS) {
+        const int next = (m0 / p.T + 1) * p.T;
+        if (t0 + 16 <= p.M) mode = t0 + 16 <= next ? 0 : (t0 >= next ? 1 : 2);
+      }
+      float rv[4];
+      if constexpr (RES) {
+        const int rbase = row0 * ldr4 + col * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          rv[r] = __builtin_bit_cast(float,
+                                     __builtin_amdgcn_raw_buffer_load_b32(rres, r < lim ? rbase + r * ldr4 : kOOB, 0, 0));
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float y = acc[i][j][r] + bv;
+        if constexpr (RES) y += rv[r];
+        if constexpr (RB) {
+          const int row = row0 + r;
+          const int rowc = row < p.M ? row : p.M - 1;
+          const int ub = p.seg ? seg_of(p.seg, p.nseg, rowc) : rowc / p.T;
+          y += p.row_bias[(size_t)ub * p.N + col];
+        }
+        if constexpr (ACT == kActRelu) y = fmaxf(y, 0.f);
+        else if constexpr (ACT == kActTanh) y = tanhf(y);
+        else if constexpr (ACT == kActGelu) y = gelu_as(y);
+        y = y * sc + sh;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, r < lim ? base + r * ldo4 : kOOB, 0,
+                                              0);
+        if constexpr (CS) {
+          const double yd = (double)y;
+          if (mode == 0) {
+            cs[j][0] += yd;
+          } else if (mode == 1) {
+            cs[j][1] += yd;
+          } else {
+            const int row = row0 + r;
+            const int next = (m0 / p.T + 1) * p.T;
+            cs[j][0] += (row < next && row < p.M) ? yd : 0.0;
+            cs[j][1] += (row >= next && row < p.M) ? yd : 0.0;
+          }
+        }
+      }
+    }
+  }
+}
+
+// gemm_colsum_reduce for the 16x16 map: lanes l, l ^ 16, l ^ 32, l ^ 48 share a column.
+template <int TN, int WM, int WN, int BM>
+__device__ __forceinline__ void gemm_colsum_reduce16(const ConvGemmArgs& p, double (*cs)[2], int m0, int n0, int wm,
+                                                     int wn, int lane, unsigned char* smem) {
+  constexpr int BN = WN * TN * 16;
+  double* red = reinterpret_cast<double*>(smem);  // [WM][2][BN]
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      double v = cs[j][u] + __shfl_xor(cs[j][u], 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16) red[(wm * 2 + u) * BN + (wn * TN + j) * 16 + lane] = v;
+    }
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid < 2 * BN) {
+    const int u = tid / BN, c = tid - u * BN;
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) v += red[(w * 2 + u) * BN + c];
+    p.colsum[((size_t)(m0 / BM) * 2 + u) * p.N + n0 + c] = v;
+  }
+}
+
+template <int TM, int TN, int WM, int WN>
+__device__ __forceinline__ void gemm_epilogue16(const ConvGemmArgs& p, f32x4 (&acc)[TM][TN], int m0, int n0, int wm,
+                                                int wn, int lane, unsigned char* smem) {
+  if (p.colsum) {
+    double cs[TN][2];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) cs[j][0] = cs[j][1] = 0.0;
+    switch (p.act) {
+      case kActRelu: gemm_epilogue_store16<TM, TN, kActRelu, false, true>(p, acc, m0, n0, wm, wn, lane, cs); break;
+      case kActTanh: gemm_epilogue_store16<TM, TN, kActTanh, false, true>(p, acc, m0, n0, wm, wn, lane, cs); break;
+      case kActGelu: gemm_epilogue_store16<TM, TN, kActGelu, false, true>(p, acc, m0, n0, wm, wn, lane, cs); break;
+      default: gemm_epilogue_store16<TM, TN, kActNone, false, true>(p, acc, m0, n0, wm, wn, lane, cs); break;
+    }
+    gemm_colsum_reduce16<TN, WM, WN, WM * TM * 16>(p, cs, m0, n0, wm, wn, lane, smem);
+    return;
+  }
+  if (p.res) {
+    switch (p.act) {
+      case kActRelu: gemm_epilogue_store16<TM, TN, kActRelu, false, false, true>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActTanh: gemm_epilogue_store16<TM, TN, kActTanh, false, false, true>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActGelu: gemm_epilogue_store16<TM, TN, kActGelu, false, false, true>(p, acc, m0, n0, wm, wn, lane); break;
+      default: gemm_epilogue_store16<TM, TN, kActNone, false, false, true>(p, acc, m0, n0, wm, wn, lane); break;
+    }
+    return;
+  }
+  if (p.row_bias) {
+    switch (p.act) {
+      case kActRelu: gemm_epilogue_store16<TM, TN, kActRelu, true>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActTanh: gemm_epilogue_store16<TM, TN, kActTanh, true>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActGelu: gemm_epilogue_store16<TM, TN, kActGelu, true>(p, acc, m0, n0, wm, wn, lane); break;
+      default: gemm_epilogue_store16<TM, TN, kActNone, true>(p, acc, m0, n0, wm, wn, lane); break;
+    }
+  } else {
+    switch (p.act) {
+      case kActRelu: gemm_epilogue_store16<TM, TN, kActRelu, false>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActTanh: gemm_epilogue_store16<TM, TN, kActTanh, false>(p, acc, m0, n0, wm, wn, lane); break;
+      case kActGelu: gemm_epilogue_store16<TM, TN, kActGelu, false>(p, acc, m0, n0, wm, wn, lane); break;
+      default: gemm_epilogue_store16<TM, TN, kActNone, false>(p, acc, m0, n0, wm, wn, lane); break;
+    }
+  }
+}
+
 // True when every 32-wide k-tile of the operand stays in one tap and segment.
 inline bool uniform_ktiles(const ConvGemmArgs& p) {
   if (p.cin % 32 != 0) return false;

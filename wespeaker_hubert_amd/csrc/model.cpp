@@ -44,6 +44,7 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
   if (arch == "ECAPA_TDNN_c512" || arch == "ECAPA_TDNN_GLOB_c512" || arch == "ECAPA_TDNN_c1024" ||
       arch == "ECAPA_TDNN_GLOB_c1024") {
     m.ecapa = true;
+    m.x3_variant = 6;  // the 256 x 256 tile on 16x16x32 MFMAs: C2 +0.8-1.2 % over 5 (r3)
     m.C = (arch.find("c1024") != std::string::npos) ? 1024 : 512;
     m.glob = arch.find("GLOB") != std::string::npos;
     WSP_CHECK(feat_dim > 0 && feat_dim % 4 == 0, "ECAPA feat_dim must be a positive multiple of 4");
@@ -257,7 +258,7 @@ void Model::set_option(const std::string& key, int value) {
               "or 4 (halo-free strips, c1024 widths; else as 3)");
     impl->res2_variant = value;
   } else if (key == "x3_variant") {
-    WSP_CHECK(value == 3 || value == 4 || value == 5, "x3_variant must be 3, 4 or 5");
+    WSP_CHECK(value >= 3 && value <= 6, "x3_variant must be 3, 4, 5 or 6 (5 on 16x16x32 MFMAs)");
     impl->x3_variant = value;
   } else {
     throw InvalidArg{"unknown option " + key};
