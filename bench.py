@@ -55,6 +55,8 @@ def dominant_symbol(precision: int, variant, N: int, K: int, role: int):
         return "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1E", 128, 128, 256
     t, bm, bn, nt = x3_tile(variant, N, K, gelu=(role == 0))  # role 0 here = HuBERT fc1 (GELU)
     sym = f"_ZN3wsp12_GLOBAL__N_112conv_gemm_x3{t}Li0ELb1ELi{role}E" + ("" if role else "Lb0E")
+    if bn == 256:  # the 256 x 256 tile (one staging set): 32x32x16 (variant 5) or 16x16x32 (6) MFMAs
+        sym += ("" if role == 0 else "Lb0E") + "Lb1ELi1E" + ("Li16E" if variant == 6 else "Li32E")
     return sym, bm, bn, nt
 HUBERT_ARCH = "HuBERT_ECAPA_GLOB_c512"  # C4: HuBERT-base front end + ECAPA_TDNN_GLOB_c512(feat_dim 768)
 HEAD_TAGS = ("layer1", "conv1x1_CxC", "res2_k3", "se", "conv_cat", "glob_ctx", "pool_linear1", "pool_linear2",
@@ -470,7 +472,7 @@ def roofline_ecapa(args, w, k, streams):
     ach = flops / (k["avg_ms"] * 1e-3) / 1e12
     x3 = args.precision == 1
     peak = BF16_MFMA_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
-    sym, bm, bn, nt = dominant_symbol(args.precision, args.x3_variant, C, C, 1)
+    sym, bm, bn, nt = dominant_symbol(args.precision, w["model"].get_option("x3_variant"), C, C, 1)
     grid = ((M + bm - 1) // bm) * (C // bn) * nt
     traffic, src = profiled_traffic(sym, grid)
     algo_bytes = 4.0 * M * C * 2 + (2 if x3 else 4) * C * C * (2 if x3 else 1)
