@@ -102,7 +102,7 @@ def _tail_pair(arch, seed, feat_dim, on=1):
 
 # feat_dim 40: stage 3 runs at F = 10, a partial 4-row frequency tile; T = 37 / 100 / 150
 # leave partial 32- / 64-frame time tiles
-@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("arch,B,T,F", [("ResNet50", 3, 100, 80), ("ResNet50", 2, 37, 40),
                                         ("ResNet101", 1, 150, 80), ("ResNet293", 2, 64, 80),
                                         ("ResNet152", 2, 45, 40)])
@@ -124,7 +124,7 @@ def test_res_tail_matches_unfused_and_oracle(arch, B, T, F, mode):
     assert np.abs(a - ref.numpy()).max() < 1e-4
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2])
 def test_res_tail_batch_rows_equal_batch_of_one(mode):
     tail, _, _ = _tail_pair("ResNet50", 42, 80, mode)
     x = torch.from_numpy(synth_feats(20, 5, 123, 80)).to(DEV)

@@ -1,7 +1,8 @@
 // Bottleneck-tail kernel check + timing (development tool, not part of the product):
-// launch_bottleneck_tail with the next conv1 fused, variant 1 (bottleneck_tail_kernel)
-// against variant 3 (tail2_kernel) on random operands; prints max |diff| of the block
-// output and of y1', the first mismatching position, and the average launch time.
+// launch_bottleneck_tail with the next conv1 fused (tail2_kernel) against the tail alone
+// (bottleneck_tail_kernel) on random operands: max |diff| of the block output, y1' against a
+// host f64 conv1 of that output (first 4096 positions), the first mismatching position, the
+// average launch time of each, and tail2_kernel's phase stamps.
 //   tail_check C B F T [reps]
 #include <hip/hip_runtime.h>
 
@@ -62,14 +63,27 @@ int main(int argc, char** argv) {
   for (auto& v : b2) v = nw(rng);
   for (auto& v : b3) v = nw(rng);
   for (auto& v : b1) v = nw(rng);
-  auto frag = [&](size_t n) {  // hi images random, lo images random small
-    std::vector<uint16_t> w(n);
-    for (auto& x : w) x = f2bf(nw(rng));
-    return w;
+  auto frag = [](size_t n) { return std::vector<uint16_t>(n); };
+  // [ks][hi, lo][tiles][64][8] images: lo = bf16(w - hi) of the same random weight
+  auto fill_frag = [&](std::vector<uint16_t>& w, int tiles) {  // tiles per plane
+    const size_t plane = (size_t)tiles * 512;
+    for (size_t ks = 0; ks < w.size() / (2 * plane); ++ks)
+      for (size_t i = 0; i < plane; ++i) {
+        const float v = nw(rng);
+        const uint16_t h = f2bf(v);
+        const uint32_t u = (uint32_t)h << 16;
+        float hf;
+        std::memcpy(&hf, &u, 4);
+        w[ks * 2 * plane + i] = h;
+        w[ks * 2 * plane + plane + i] = f2bf(v - hf);
+      }
   };
-  const std::vector<uint16_t> w2 = frag((size_t)9 * C / 16 * 2 * (C / 32) * 512);
-  const std::vector<uint16_t> w3 = frag((size_t)C / 16 * 2 * (4 * C / 32) * 512);
-  const std::vector<uint16_t> w1 = frag((size_t)4 * C / 16 * 2 * (C / 32) * 512);
+  std::vector<uint16_t> w2 = frag((size_t)9 * C / 16 * 2 * (C / 32) * 512);
+  std::vector<uint16_t> w3 = frag((size_t)C / 16 * 2 * (4 * C / 32) * 512);
+  std::vector<uint16_t> w1 = frag((size_t)4 * C / 16 * 2 * (C / 32) * 512);
+  fill_frag(w2, C / 32);
+  fill_frag(w3, 4 * C / 32);
+  fill_frag(w1, C / 32);
   float *dy1 = dev(y1), *dres = dev(res), *db2 = dev(b2), *db3 = dev(b3), *db1 = dev(b1);
   uint16_t *dw2 = dev(w2), *dw3 = dev(w3), *dw1 = dev(w1);
   float *out[2], *y1n[2];
@@ -85,16 +99,17 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dst, (size_t)nblk * 16 * 8));
   CK(hipMemset(dst, 0, (size_t)nblk * 16 * 8));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dst, sizeof(dst)));
-  const int vars[2] = {1, 3};
+  const int vars[2] = {0, 1};  // 0: tail alone (w1n null), 1: with the next conv1 (tail2_kernel)
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   for (int i = 0; i < 2; ++i) {
     BottleneckTailArgs a{dy1, dres, out[i], B, F, T, dw2, db2, dw3, db3};
-    a.w1n = dw1;
-    a.b1n = db1;
-    a.y1n = y1n[i];
-    a.variant = vars[i];
+    if (vars[i]) {
+      a.w1n = dw1;
+      a.b1n = db1;
+      a.y1n = y1n[i];
+    }
     launch_bottleneck_tail(a, C, 0);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0, 0));
@@ -152,6 +167,35 @@ int main(int argc, char** argv) {
     std::printf(" | block %.0f, span %llu cycles, %d blocks\n", tot, t1 - t0, nblk);
   }
   cmp("out", out, npos * 4 * C, 4 * C);
-  cmp("y1n", y1n, npos * C, C);
+  {  // y1' = relu(b1 + W1 . out) on the host (W1 = hi + lo of the pack_frag image)
+    const size_t np = std::min<size_t>(npos, 4096);
+    std::vector<float> o(np * 4 * C), yg(np * C);
+    CK(hipMemcpy(o.data(), out[1], o.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(yg.data(), y1n[1], yg.size() * 4, hipMemcpyDeviceToHost));
+    auto bf = [](uint16_t v) {
+      const uint32_t u = (uint32_t)v << 16;
+      float f;
+      std::memcpy(&f, &u, 4);
+      return f;
+    };
+    std::vector<double> W((size_t)C * 4 * C);
+    const int NT1 = C / 32;
+    for (int ks = 0; ks < 4 * C / 16; ++ks)
+      for (int t = 0; t < NT1; ++t)
+        for (int l = 0; l < 64; ++l)
+          for (int e = 0; e < 8; ++e) {
+            const size_t hi = ((((size_t)ks * 2 + 0) * NT1 + t) * 64 + l) * 8 + e;
+            const size_t lo = ((((size_t)ks * 2 + 1) * NT1 + t) * 64 + l) * 8 + e;
+            W[(size_t)(t * 32 + (l & 31)) * 4 * C + 16 * ks + 8 * (l >> 5) + e] = (double)bf(w1[hi]) + bf(w1[lo]);
+          }
+    double mx = 0;
+    for (size_t q = 0; q < np; ++q)
+      for (int n = 0; n < C; ++n) {
+        double acc = b1[n];
+        for (int k = 0; k < 4 * C; ++k) acc += W[(size_t)n * 4 * C + k] * o[q * 4 * C + k];
+        mx = std::fmax(mx, std::fabs(std::fmax(acc, 0.0) - yg[q * C + n]));
+      }
+    std::printf("y1n vs host f64 conv1 (%zu positions): max |diff| %.3g\n", np, mx);
+  }
   return 0;
 }

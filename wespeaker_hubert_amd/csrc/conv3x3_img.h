@@ -49,7 +49,6 @@ struct BottleneckTailArgs {
   const void* w1n = nullptr;
   const float* b1n = nullptr;
   float* y1n = nullptr;
-  int variant = 1;  // 3: 128 planes with the next conv1 on tail128_kernel (both runs per wave in phase 2)
 };
 bool bottleneck_tail_supported(int C);
 void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s);

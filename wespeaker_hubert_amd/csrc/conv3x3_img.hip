@@ -235,21 +235,13 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void conv3x3_img_kernel(cons
 // its k-loop), then b3 + residual, ReLU, store.  y2 never exists in memory: per
 // position the HBM traffic is y1 (halo re-reads mostly L2 hits) + res + out instead
 // of conv2's y1 + y2 and conv3's y2 + res + out.
-template <int C, int FB, int TB, int WN, int MINB, int NC, bool FUSE1, int P1, int PM>
+template <int C, int FB, int TB, int WN, int MINB, int NC, int P1, int PM>
 __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(const BottleneckTailArgs p) {
   using G = Img<C, FB, TB, WN>;
   constexpr int TN = G::TN, PT = G::PT;
   constexpr int C4 = 4 * C, NT3 = C4 / 32, KS3 = C / 16;
   constexpr int NTW = NT3 / WN, NCH = NTW / NC;  // conv3 column tiles per wave, chunks
   static_assert(NTW % NC == 0 && KS3 % 2 == 0, "bottleneck_tail chunks");
-  // FUSE1: a chunk's conv3 outputs of both partner waves (CH channels) are the K block of
-  // the next conv1: staged in LDS as bf16 hi / lo rows [position][CH] (Img-style swizzle)
-  constexpr int CH = WN * NC * 32, KK = CH / 16, CBR = 2 * CH, NPR = G::NW / WN;
-  constexpr int NT1 = C / 32, TN1 = NT1 / WN;  // next conv1: output tiles, per wave
-  static_assert(!FUSE1 || (KK % 2 == 0 && 2 * NPR * 32 * CBR <= G::LDS), "conv1 chunk buffer");
-  // two chunk buffers where the image's LDS holds them: one barrier per chunk instead of two
-  constexpr int CBUF = 2 * NPR * 32 * CBR;
-  constexpr bool CB2 = 2 * CBUF <= G::LDS;
   static_assert(WN == 1 || G::IR * G::RB * 2 >= G::NW / WN * KS3 * 2048, "y2 exchange must fit the image");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* xhi = smem;
@@ -439,7 +431,7 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
     }
   }
 
-  // ---- phase 2: conv3 over NCH chunks of NC column tiles (+ FUSE1: the next conv1 on each chunk)
+  // ---- phase 2: conv3 over NCH chunks of NC column tiles
   const size_t obase = (size_t)b * plane * C4;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out + obase);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res + obase);
@@ -449,45 +441,9 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
     const int t = tw + (r & 3) + 8 * (r >> 2);
     return f < p.F && t < p.T ? ((f * p.T + t) * C4 + col) * 4 : kOOB;
   };
-  // FUSE1 state: next-conv1 accumulators (this wave's TN1 output tiles), W1 fragment ring,
-  // chunk buffer addressing (swizzle as Img's for 64 / 128 / 256-B rows)
-  f32x16 acc1[FUSE1 ? TN1 : 1];
-  if constexpr (FUSE1) {
-#pragma unroll
-    for (int j = 0; j < TN1; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc1[j][r] = 0.f;
-    if constexpr (WN == 2) __syncthreads();  // partners are done reading the y2 exchange
-  }
-  auto cbsw = [](int r) { return CBR == 64 ? ((r >> 2) & 3) : CBR == 128 ? ((r >> 1) & 7) : (r & 15); };
-  auto cbaddr = [&](int prow, int c16) { return prow * CBR + ((c16 ^ cbsw(prow)) << 4); };
-  const __amdgpu_buffer_rsrc_t rw1 = make_rsrc(FUSE1 ? p.w1n : p.w3);
-  // k-step kk of chunk `chunk`'s K block -> global k-step of W1 (4C-deep): the block holds
-  // partner 0's NC tiles, then partner 1's
-  auto ks1of = [&](int chunk, int kk) {
-    const int part = kk / (2 * NC), off = kk - part * 2 * NC;
-    return (part * NTW + chunk * NC) * 2 + off;
-  };
-  auto w1load = [&](int chunk, int kk, bf16x8 (&bh)[TN1], bf16x8 (&bl)[TN1]) {
-    const bool ok = chunk < NCH;
-    const int ks = ks1of(ok ? chunk : 0, kk);
-#pragma unroll
-    for (int j = 0; j < TN1; ++j) {
-      const int o = ((ks * 2 * NT1 + wn * TN1 + j) * 64 + lane) * 16;
-      bh[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1, ok ? o : kOOB, 0, 0));
-      bl[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1, ok ? o + NT1 * 1024 : kOOB, 0, 0));
-    }
-  };
 #pragma unroll 1
   for (int chunk = 0; chunk < NCH; ++chunk) {
     const int cb = (wn * NTW + chunk * NC) * 32 + r32;  // column of tile 0
-    unsigned char* cbhi = smem + (CB2 ? (chunk & 1) * CBUF : 0);
-    unsigned char* cblo = cbhi + NPR * 32 * CBR;
-    bf16x8 u0h[FUSE1 ? TN1 : 1], u0l[FUSE1 ? TN1 : 1], u1h[FUSE1 ? TN1 : 1], u1l[FUSE1 ? TN1 : 1];
-    if constexpr (FUSE1) {  // the chunk's first two W1 k-steps land during its conv3
-      w1load(chunk, 0, u0h, u0l);
-      w1load(chunk, 1, u1h, u1l);
-    }
     float rv[NC][16];
 #pragma unroll
     for (int j = 0; j < NC; ++j)
@@ -537,95 +493,30 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
       for (int r = 0; r < 16; ++r) {
         const float y = fmaxf(a3[j][r] + bv + rv[j][r], 0.f);
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, roff(col, r), 0, 0);
-        if constexpr (FUSE1) {
-          // chunk buffer row = position, column (wn * NC + j) * 32 + r32; lanes l, l ^ 1 hold
-          // columns c, c ^ 1: the even lane stores both hi halves, the odd lane both lo halves
-          const __bf16 hh = (__bf16)y;
-          const __bf16 ll = (__bf16)(y - (float)hh);
-          const unsigned short hb = __builtin_bit_cast(unsigned short, hh);
-          const unsigned short lb = __builtin_bit_cast(unsigned short, ll);
-          const unsigned send = (lane & 1) ? hb : lb;
-          const unsigned recv = (unsigned)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
-          const int prow = pr * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const int cc = (wn * NC + j) * 32 + (r32 & ~1);
-          const int a = cbaddr(prow, cc >> 3) + (cc & 7) * 2;
-          if (lane & 1)
-            *reinterpret_cast<unsigned*>(cblo + a) = recv | ((unsigned)lb << 16);
-          else
-            *reinterpret_cast<unsigned*>(cbhi + a) = (unsigned)hb | (recv << 16);
-        }
-      }
-    }
-    if constexpr (FUSE1) {
-      __syncthreads();  // both partners' halves of the chunk are in LDS
-#pragma unroll
-      for (int kk = 0; kk < KK; kk += 2) {
-        bf16x8 ah, al;
-        {
-          const int a = cbaddr(pr * 32 + r32, 2 * kk + h);
-          ah = *reinterpret_cast<const bf16x8*>(cbhi + a);
-          al = *reinterpret_cast<const bf16x8*>(cblo + a);
-        }
-#pragma unroll
-        for (int j = 0; j < TN1; ++j) {
-          acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, u0h[j], acc1[j], 0, 0, 0);
-          acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, u0l[j], acc1[j], 0, 0, 0);
-          acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, u0h[j], acc1[j], 0, 0, 0);
-        }
-        if (kk + 2 < KK) w1load(chunk, kk + 2, u0h, u0l);
-        __builtin_amdgcn_sched_barrier(0);
-        {
-          const int a = cbaddr(pr * 32 + r32, 2 * (kk + 1) + h);
-          ah = *reinterpret_cast<const bf16x8*>(cbhi + a);
-          al = *reinterpret_cast<const bf16x8*>(cblo + a);
-        }
-#pragma unroll
-        for (int j = 0; j < TN1; ++j) {
-          acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, u1h[j], acc1[j], 0, 0, 0);
-          acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, u1l[j], acc1[j], 0, 0, 0);
-          acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, u1h[j], acc1[j], 0, 0, 0);
-        }
-        if (kk + 3 < KK) w1load(chunk, kk + 3, u1h, u1l);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr (!CB2) __syncthreads();  // the chunk buffer is rewritten by the next chunk
-    }
-  }
-  if constexpr (FUSE1) {
-    // y1' = relu(acc1 + b1') -> y1n [B][F][T][C]
-    const __amdgpu_buffer_rsrc_t ry = make_rsrc(p.y1n + (size_t)b * plane * C);
-#pragma unroll
-    for (int j = 0; j < TN1; ++j) {
-      const int col = (wn * TN1 + j) * 32 + r32;
-      const float bv = p.b1n[col];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int t = tw + (r & 3) + 8 * (r >> 2);
-        const float y = fmaxf(acc1[j][r] + bv, 0.f);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ry,
-                                              f < p.F && t < p.T ? ((f * p.T + t) * C + col) * 4 : kOOB, 0, 0);
       }
     }
   }
 }
 
 // Bottleneck tail with the next conv1 fused, every wave on TWO position runs in both phases
-// (option res_tail 3, r3; 64 / 128 planes).  bottleneck_tail_kernel's fused forms fetch, per
-// chunk and wave, W3 / W1 fragments that feed one 32-position run (and for 64 planes also
-// conv2's W2); here each of the 4 waves runs conv2, conv3 and the next conv1 for a PAIR of runs
-// and 1 / GW of the columns, so every weight fragment fetched from L2 feeds two MFMA triples.
-// 128 planes: a 2 x 32 tile (one run pair, GW = 4 column groups); 64 planes: 4 x 32 (two run
-// pairs, GW = 2).  y2 stays in LDS as MFMA A fragments ([run][k-step][hi, lo][64 lanes] x 16 B,
-// 32 KB) read per k-step.  Chunk c = conv3 column tiles GW c .. GW c + GW - 1 (wave (pair, g):
-// tile GW c + g) = the next conv1's k-steps 2 GW c .. 2 GW c + 2 GW - 1; its LDS buffer holds
-// those channels for every run.  Issue order keeps HBM latency off the critical path: chunk c +
-// 1's residual (and bias) goes out right behind chunk c's last W1 fetch (chunk 0's at the start
-// of conv2's last W2 ring group, conv2's bias with the patch), so the first wait covering it
-// comes RD3 + RD1 k-steps later (bottleneck_tail_kernel issues the residual at the chunk start
-// and waits on it 2 k-steps later, and its epilogue's bias load drains every prefetch).  RD3 /
-// RD1: W3 / W1 ring depths.  (Holding the outputs in registers to store them later as well
-// spilled; an in-place variant through the accumulators was miscompiled: one element stored 16
-// times.)
+// (option res_tail 1, default, r3; 32 / 64 / 128 planes).  The first fused form (the r3
+// bottleneck_tail_kernel with FUSE1, since removed) fetched, per chunk and wave, W3 / W1
+// fragments that fed one 32-position run (for 64 planes also conv2's W2); here each of the 4
+// waves runs conv2, conv3 and the next conv1 for a PAIR of runs and 1 / GW of the columns, so
+// every weight fragment fetched from L2 feeds two MFMA triples.  128 planes: a 2 x 32 tile (one
+// run pair, GW = 4 column groups); 64 planes: 4 x 32 (two run pairs, GW = 2); 32 planes: 8 x 32
+// (four run pairs, GW = 1).  y2 stays in LDS as MFMA A fragments ([run][k-step][hi, lo][64
+// lanes] x 16 B, 32 KB) read per k-step.  Chunk c = conv3 column tiles GW c .. GW c + GW - 1
+// (wave (pair, g): tile GW c + g) = the next conv1's k-steps 2 GW c .. 2 GW c + 2 GW - 1; its
+// LDS buffer holds those channels for every run.  Issue order keeps HBM latency off the
+// critical path: chunk c + 1's residual (and bias) goes out right behind chunk c's last W1 fetch
+// (chunk 0's at the start of conv2's last W2 ring group, conv2's bias with the patch), so the
+// first wait covering it comes RD3 + RD1 k-steps later (the first form issued the residual at
+// the chunk start and waited on it 2 k-steps later, and its epilogue's bias load drained every
+// prefetch).  RD3 / RD1: W3 / W1 ring depths.  (Holding the outputs in registers to store them
+// later as well spilled; an in-place variant through the accumulators was miscompiled: one
+// element stored 16 times.)  Measured against the first form: 128 planes 0.391 -> 0.364 ms,
+// 64 planes 0.548 -> 0.468 ms, 32 planes 0.828 -> 0.785 ms per launch (B = 64, tools/tail_check).
 
 // dynamic LDS of tail2_kernel: the patch image, later y2 fragments + the chunk buffer
 template <int C>
@@ -956,18 +847,13 @@ void launch_conv3x3_img(const Conv3x3Args& p, int C, hipStream_t s) {
 }
 
 namespace {
-template <int C, int FB, int TB, int WN, int MINB, int NC, int NC1 = NC, int MINB1 = MINB, int PM = 1>
+template <int C, int FB, int TB, int WN, int MINB, int NC, int PM = 1>
 void launch_tail_k(const BottleneckTailArgs& p, hipStream_t s) {
   using G = Img<C, FB, TB, WN>;
   // W2 k-steps in flight in phase 1: 4 where the register budget (MINB) leaves room
-  constexpr int P1F = G::KS % 4 == 0 && MINB1 <= 2 ? 4 : 2, P1U = G::KS % 4 == 0 && MINB <= 2 ? 4 : 2;
+  constexpr int P1 = G::KS % 4 == 0 && MINB <= 2 ? 4 : 2;
   const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + TB - 1) / TB);
-  if (p.w1n)
-    hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB1, NC1, true, P1F, PM>), dim3(nblk), dim3(G::NT), G::LDS,
-                       s, p);
-  else
-    hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB, NC, false, P1U, PM>), dim3(nblk), dim3(G::NT), G::LDS,
-                       s, p);
+  hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB, NC, P1, PM>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
 }
 
 template <int C, int P1, int RD3, int RD1>
@@ -989,25 +875,20 @@ void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s) {
   WSP_CHECK((long long)p.F * p.T * 4 * C * 4 < (long long)kOOB, "bottleneck_tail: utterance exceeds 2 GiB");
   WSP_CHECK(!p.w1n || (p.b1n && p.y1n && p.y1n != p.out && p.y1n != p.y1 && p.y1n != p.res),
             "bottleneck_tail: next conv1 needs bias and a separate output");
-  // <C, FB, TB, WN, MINB, NC[, NC and MINB with the next conv1]>
-  if (C == 32 && p.w1n && p.variant == 3)
-    launch_tail2<32, 2, 2, 1>(p, s);  // 256 positions (8 runs), 4 waves, 64 KB: 2 blocks / CU
-  else if (C == 32 && p.w1n)
-    launch_tail_k<32, 4, 32, 1, 3, 1>(p, s);  // 128 positions, 4 waves, 26 KB image: 3 blocks / CU
-  else if (C == 32)
+  if (p.w1n) {  // with the next block's conv1: every wave on two position runs (tail2_kernel)
+    if (C == 32)
+      launch_tail2<32, 2, 2, 1>(p, s);  // 8 x 32 positions, 4 waves, 64 KB: 2 blocks / CU
+    else if (C == 64)
+      launch_tail2<64, 4, 4, 2>(p, s);  // 4 x 32 positions, 64 KB
+    else
+      launch_tail2<128, 4, 4, 4>(p, s);  // 2 x 32 positions, 68 KB
+  } else if (C == 32) {  // <C, FB, TB, WN, MINB, NC[, PM]>
     launch_tail_k<32, 4, 64, 1, 4, 1>(p, s);  // 256 positions, 8 waves, 50 KB image: 2 blocks / CU
-  else if (C == 64 && p.w1n && p.variant == 3)
-    launch_tail2<64, 4, 4, 2>(p, s);
-  else if (C == 64)  // (a 2 x 32 tile: C3 -1.3 %)
-    launch_tail_k<64, 4, 32, 1, 3, 2, 1, 2>(p, s);  // 128 positions, 4 waves, 51 KB image: 3 blocks / CU
-  else if (p.w1n && p.variant == 3)
-    launch_tail2<128, 4, 4, 4>(p, s);
-  else if (p.w1n)
-    // with the next conv1 (per-chunk barriers), two independent blocks per CU: C3 +1.5 % over the
-    // 4 x 32 tile (one 102 KB block per CU)
-    launch_tail_k<128, 2, 32, 2, 2, 2, 1, 2, 2>(p, s);  // 64 positions, 4 waves, 70 KB image: 2 blocks / CU
-  else
-    launch_tail_k<128, 4, 32, 2, 2, 2, 1, 2, 2>(p, s);  // 128 positions, 8 waves (2 per position run), 102 KB image
+  } else if (C == 64) {  // (a 2 x 32 tile: C3 -1.3 %)
+    launch_tail_k<64, 4, 32, 1, 3, 2>(p, s);  // 128 positions, 4 waves, 51 KB image: 3 blocks / CU
+  } else {
+    launch_tail_k<128, 4, 32, 2, 2, 2, 2>(p, s);  // 128 positions, 8 waves (2 per position run), 102 KB image
+  }
   WSP_HIP(hipGetLastError());
 }
 

@@ -318,16 +318,22 @@ void launch_x3_k(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hi
 
 template <int WM, int WN, int TM, int TN, bool SWZ = false, int NSET = 2, int MF = 32>
 void launch_x3_tile(const ConvGemmArgs& p, const __bf16* whi, const __bf16* wlo, hipStream_t s) {
-  if (p.conv2d) {
-    launch_x3_k<WM, WN, TM, TN, kACat, true, 0, true, SWZ, NSET, MF>(p, whi, wlo, s);
-    return;
+  // the 16x16 form serves 1-D convs with one A operand (ECAPA, HuBERT): its 2-D and added-operand
+  // kernels are not instantiated (t_4x2_2x4_mf16 routes those GEMMs to the 32x32 form)
+  if constexpr (MF == 32) {
+    if (p.conv2d) {
+      launch_x3_k<WM, WN, TM, TN, kACat, true, 0, true, SWZ, NSET, MF>(p, whi, wlo, s);
+      return;
+    }
   }
   const bool uni = uniform_ktiles(p);
-  if (p.amode == kAAdd) {
-    if (uni)
-      launch_x3_k<WM, WN, TM, TN, kAAdd, true, 0, false, SWZ, NSET, MF>(p, whi, wlo, s);
-    else
-      launch_x3_k<WM, WN, TM, TN, kAAdd, false, 0, false, SWZ, NSET, MF>(p, whi, wlo, s);
+  if (MF == 32 && p.amode == kAAdd) {
+    if constexpr (MF == 32) {
+      if (uni)
+        launch_x3_k<WM, WN, TM, TN, kAAdd, true, 0, false, SWZ, NSET, MF>(p, whi, wlo, s);
+      else
+        launch_x3_k<WM, WN, TM, TN, kAAdd, false, 0, false, SWZ, NSET, MF>(p, whi, wlo, s);
+    }
   } else if (!uni) {
     launch_x3_k<WM, WN, TM, TN, kACat, false, 0, false, SWZ, NSET, MF>(p, whi, wlo, s);
   } else if (p.role == 1) {

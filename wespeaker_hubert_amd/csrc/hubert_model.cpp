@@ -11,6 +11,8 @@
 //   Featurizer + length match          accumulated inside each hidden-state LN
 // Parameters arrive under the reference checkpoint's names
 // ("frontend.upstream.upstream.model." + fairseq names, "frontend.featurizer.weights").
+#include <cstring>
+
 #include "attn.h"
 #include "model_impl.h"
 
@@ -262,7 +264,16 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
     g.seg = oseg;  // taps==1 projections pass null: row-local, no utterance structure needed
     g.iseg = iseg;
     g.nseg = nseg;
-    run(tag, 2.0 * rows * (gcols ? (double)cw.N * kPosGin / kPosGout : cw.N) * cw.K, s, [&] { launch(g, cw, s); });
+    // the long-K / GELU GEMMs (CNN, fc1, fc2) on the 16x16x32 form of the 256 x 256 tile (r3 A/B:
+    // CNN -2 %, fc1 -3 %, fc2 -6 % per launch); QKV / out_proj measured slower on it and stay on 32x32
+    const bool mf16 = x3_variant == 5 && (std::strncmp(tag, "h_cnn", 5) == 0 || std::strcmp(tag, "h_fc1") == 0 ||
+                                          std::strcmp(tag, "h_fc2") == 0);
+    run(tag, 2.0 * rows * (gcols ? (double)cw.N * kPosGin / kPosGout : cw.N) * cw.K, s, [&] {
+      if (precision == 1)
+        launch_conv_gemm_x3(g, cw.whi, cw.wlo, mf16 ? 6 : x3_variant, s);
+      else
+        launch(g, cw, s);
+    });
   };
   auto ln = [&](const char* tag, const float* in, const float* add, float* out, int rows, int D, const float* gm,
                 const float* bt, int layer) {

@@ -230,9 +230,7 @@ void Model::set_option(const std::string& key, int value) {
     WSP_CHECK(value == 0 || value == 1, "res_prefetch must be 0 or 1");
     impl->res_prefetch = value;
   } else if (key == "res_tail") {
-    WSP_CHECK(value >= 0 && value <= 3,
-              "res_tail must be 0 (off), 1 (tail + next conv1), 2 (tail alone) or 3 (as 1, 64 / 128-plane tails "
-              "on tail2_kernel)");
+    WSP_CHECK(value >= 0 && value <= 2, "res_tail must be 0 (off), 1 (tail + next conv1) or 2 (tail alone)");
     impl->res_tail = value;
   } else if (key == "cat_gate") {
     WSP_CHECK(value == 0 || value == 1, "cat_gate must be 0 or 1");

@@ -147,9 +147,9 @@ struct Model::Impl {
   int res_prefetch = 1;  // ResNet 1x1 residual convs: residual loaded ahead of the last k-tiles (option "res_prefetch")
   // ResNet bottleneck conv2 + conv3 (+ residual) of stride-1 blocks with planes 32 / 64 / 128 in one
   // launch, y2 kept in registers (conv3x3_img.hip bottleneck_tail; option "res_tail"): 1 = also the
-  // next block's conv1 on the tail's output while it is on chip, 2 = the tail alone, 0 = off;
-  // 3 = as 1 with the 64 / 128-plane fused tails on tail2_kernel (two position runs per wave)
-  int res_tail = 3;
+  // next block's conv1 on the tail's output while it is on chip (tail2_kernel: two position runs
+  // per wave), 2 = the tail alone, 0 = off
+  int res_tail = 1;
   bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
   int res2_variant = 4;  // res2_chain.hip kernel variant (option "res2_variant"; 4 = halo-free strips, C2 1.48 -> 1.24 ms/step; c512 widths run 3)
   ConvW conv, pool1, pool2;
@@ -687,7 +687,7 @@ struct Model::Impl {
             // the tail does not read)
             const RBlock* nx = (size_t)ib < rblocks.size() ? &rblocks[ib] : nullptr;
             // (the next block must run the tail too: its conv2 then reads y1 from either buffer)
-            const bool fuse1 = res_tail != 2 && nx && nx->w1frag && nx->planes == rb.planes && nx->w3acc &&
+            const bool fuse1 = res_tail == 1 && nx && nx->w1frag && nx->planes == rb.planes && nx->w3acc &&
                                nx->stride == 1 && img_ok(nx->c2, nx->planes);
             BottleneckTailArgs a{y1, res, o, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.w3acc, rb.c3.bias};
             float* y1n = y1 == Y1 ? Y2 : Y1;
@@ -695,7 +695,6 @@ struct Model::Impl {
               a.w1n = nx->w1frag;
               a.b1n = nx->c1.bias;
               a.y1n = y1n;
-              a.variant = res_tail;
             }
             const double pos = (double)nb * Fi * Ti;
             run(kTl[li], 2.0 * pos * (rb.c2.N * rb.c2.K + rb.c3.N * rb.c3.K + (fuse1 ? nx->c1.N * nx->c1.K : 0)), s,
