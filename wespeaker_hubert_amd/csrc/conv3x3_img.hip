@@ -691,7 +691,17 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
       *reinterpret_cast<bf16x8*>(y2s + o) = vh;
       *reinterpret_cast<bf16x8*>(y2s + o + 1024) = vl;
     }
-  __syncthreads();
+  // GW = 1 (32 planes): a wave reads back only the y2 / chunk-buffer rows of its own runs, so
+  // ordering its own LDS accesses replaces the workgroup barriers
+  auto sync = [] {
+    if constexpr (GW > 1) {
+      __syncthreads();
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  };
+  sync();
   WSP_TAIL_STAMP(3);
 
   auto read_y2 = [&](int ks, bf16x8 (&ah)[2], bf16x8 (&al)[2]) {
@@ -750,7 +760,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
       else w3load(c + 1, q + RD3 - KS3, ch_[q % RD3], cl_[q % RD3]);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (c > 0) __syncthreads();  // every wave is done reading chunk c - 1 from the buffer
+    if (c > 0) sync();  // every wave is done reading chunk c - 1 from the buffer
     // epilogue: out = relu(a3 + b3 + res) -> HBM and as bf16 hi / lo rows of the chunk buffer.
     // The first wait covering these stores is the one on the W1 fetch that conv1's k-step 0
     // issues after them, RD1 k-steps later (stores count in vmcnt like loads)
@@ -780,7 +790,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
         }
       }
     }
-    __syncthreads();  // the chunk's GW x 32 channels of every run are in LDS
+    sync();  // the chunk's GW x 32 channels of every run are in LDS
     // next conv1: k-steps KB c .. KB c + KB - 1, output tile g, the wave's two runs
     read_cb(0, ah[0], al[0]);
 #pragma unroll
