@@ -83,6 +83,17 @@ def test_unknown_arch_is_an_error():
     assert lib.wsp_model_create(b"NOPE", 80, 192, 0, 0, ctypes.byref(h)) != 0
 
 
+def test_resnet_feat_dim_must_be_a_multiple_of_8():
+    """resnet.py:124 sizes seg_1 for int(feat_dim / 8) frequency rows while the convs keep
+    ceil(feat_dim / 8): the reference only runs for multiples of 8, so the C-ABI refuses the rest."""
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.wsp_model_create(b"ResNet34", 60, 256, 0, 0, ctypes.byref(h)) != 0
+    assert b"multiple of 8" in lib.wsp_last_error()
+    assert lib.wsp_model_create(b"ResNet34", 72, 256, 0, 0, ctypes.byref(h)) == 0
+    lib.wsp_model_destroy(h)
+
+
 def test_option_defaults_and_streams_workspace():
     """Host-only: per-architecture option defaults (wsp_model_get_option) and the
     workspace of a split batch ("streams": one 256-B-granular slice per range)."""

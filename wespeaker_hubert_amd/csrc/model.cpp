@@ -58,7 +58,9 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
         {"ResNet293", {true, {10, 20, 64, 3}}}};
     auto it = kRes.find(arch);
     WSP_CHECK(it != kRes.end(), "unsupported arch " + arch);
-    WSP_CHECK(feat_dim >= 8, "ResNet feat_dim must be >= 8");
+    // resnet.py:124 sizes the pooling for int(feat_dim / 8) frequency rows while stage 4 keeps
+    // ceil(feat_dim / 8): the reference model only runs for multiples of 8
+    WSP_CHECK(feat_dim >= 8 && feat_dim % 8 == 0, "ResNet feat_dim must be a positive multiple of 8");
     m.ecapa = false;
     m.x3_variant = 4;  // 256 x 128 swizzled: with the residual prefetch (ROLE 2) +1.3 % C3 over variant 3 (r2c)
     m.streams = 2;     // two utterance ranges in flight: ResNet293 C3 +8.6 %
