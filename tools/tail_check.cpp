@@ -120,6 +120,40 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     std::printf("variant %d: %.4f ms per launch\n", vars[i], ms / reps);
   }
+  {  // other ring depths of tail2_kernel <C, W2 ring, W3 ring, W1 ring> (timing; the last one's
+     // outputs are the ones compared below)
+    BottleneckTailArgs a{dy1, dres, out[1], B, F, T, dw2, db2, dw3, db3};
+    a.w1n = dw1;
+    a.b1n = db1;
+    a.y1n = y1n[1];
+    auto timeit = [&](const char* name, auto go) {
+      go();
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0, 0));
+      for (int r = 0; r < reps; ++r) go();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      std::printf("tail2 %s: %.4f ms per launch\n", name, ms / reps);
+    };
+    for (int round = 0; round < 3; ++round) {  // interleaved rounds: the first launches of a
+    std::printf("round %d\n", round);           // process run slower (clock / cache warm-up)
+    if (C == 128) {
+      timeit("<128, 4, 4, 4>", [&] { launch_tail2<128, 4, 4, 4>(a, 0); });
+      timeit("<128, 8, 4, 6>", [&] { launch_tail2<128, 8, 4, 6>(a, 0); });
+      timeit("<128, 8, 4, 4>", [&] { launch_tail2<128, 8, 4, 4>(a, 0); });
+    } else if (C == 64) {
+      timeit("<64, 4, 4, 2>", [&] { launch_tail2<64, 4, 4, 2>(a, 0); });
+      timeit("<64, 12, 4, 2>", [&] { launch_tail2<64, 12, 4, 2>(a, 0); });
+      timeit("<64, 6, 4, 3>", [&] { launch_tail2<64, 6, 4, 3>(a, 0); });
+      timeit("<64, 6, 4, 2>", [&] { launch_tail2<64, 6, 4, 2>(a, 0); });
+    } else {
+      timeit("<32, 6, 2, 1>", [&] { launch_tail2<32, 6, 2, 1>(a, 0); });
+      timeit("<32, 2, 2, 1>", [&] { launch_tail2<32, 2, 2, 1>(a, 0); });
+    }
+    }
+  }
   auto cmp = [&](const char* name, float* const* d, size_t n, int ch) {
     std::vector<float> h0(n), h1(n);
     CK(hipMemcpy(h0.data(), d[0], n * 4, hipMemcpyDeviceToHost));

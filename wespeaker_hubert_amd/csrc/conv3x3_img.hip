@@ -515,8 +515,8 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
 // the chunk start and waited on it 2 k-steps later, and its epilogue's bias load drained every
 // prefetch).  RD3 / RD1: W3 / W1 ring depths.  (Holding the outputs in registers to store them
 // later as well spilled; an in-place variant through the accumulators was miscompiled: one
-// element stored 16 times.)  Measured against the first form: 128 planes 0.391 -> 0.364 ms,
-// 64 planes 0.548 -> 0.468 ms, 32 planes 0.828 -> 0.785 ms per launch (B = 64, tools/tail_check).
+// element stored 16 times.)  Against the first form: C3 ResNet293 1 622 -> 1 732 emb/s
+// (interleaved model-level A/B).
 
 // dynamic LDS of tail2_kernel: the patch image, later y2 fragments + the chunk buffer
 template <int C>
@@ -886,12 +886,15 @@ void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s) {
   WSP_CHECK(!p.w1n || (p.b1n && p.y1n && p.y1n != p.out && p.y1n != p.y1 && p.y1n != p.res),
             "bottleneck_tail: next conv1 needs bias and a separate output");
   if (p.w1n) {  // with the next block's conv1: every wave on two position runs (tail2_kernel)
+    // <C, W2 ring depth, W3 ring, W1 ring>; 128 planes with an 8-deep W2 ring: 0.323 -> 0.314 ms
+    // per launch (tools/tail_check, B = 64, interleaved rounds); deeper W2 / W1 rings for 32 / 64
+    // planes measured within 0.5 %
     if (C == 32)
       launch_tail2<32, 2, 2, 1>(p, s);  // 8 x 32 positions, 4 waves, 64 KB: 2 blocks / CU
     else if (C == 64)
       launch_tail2<64, 4, 4, 2>(p, s);  // 4 x 32 positions, 64 KB
     else
-      launch_tail2<128, 4, 4, 4>(p, s);  // 2 x 32 positions, 68 KB
+      launch_tail2<128, 8, 4, 4>(p, s);  // 2 x 32 positions, 68 KB
   } else if (C == 32) {  // <C, FB, TB, WN, MINB, NC[, PM]>
     launch_tail_k<32, 4, 64, 1, 4, 1>(p, s);  // 256 positions, 8 waves, 50 KB image: 2 blocks / CU
   } else if (C == 64) {  // (a 2 x 32 tile: C3 -1.3 %)
