@@ -155,9 +155,9 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *                  ahead of the last two k-tiles (default), 0 = in the epilogue (bit-identical)
  *   "res_tail"     ResNet: 2 = the bottleneck conv2 (3x3) + conv3 (1x1) + residual + ReLU of
  *                  stride-1 blocks with 32 / 64 / 128 planes in one launch, conv2's output kept in
- *                  registers; 1 = that, plus the next block's conv1 on the output while it is on chip;
- *                  3 = as 1, the 64 / 128-plane fused tails with every wave on two position runs
- *                  (tail2_kernel, default); 0 = conv2, conv3 and conv1 as separate launches through HBM
+ *                  registers; 1 = that, plus the next block's conv1 on the output while it is on chip,
+ *                  every wave on two position runs (tail2_kernel, default); 0 = conv2, conv3 and
+ *                  conv1 as separate launches through HBM
  *   "cat_gate"     ECAPA-TDNN: 1 = conv_cat on [out2, out3, out4 - out3] with weights
  *                  [W_a, W_b + W_c, W_c], so the last SE block stores only its gated branch
  *                  (default; equal to 0 up to rounding, ~1e-6), 0 = conv_cat on [out2, out3, out4]
