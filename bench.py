@@ -168,6 +168,26 @@ def resnet_1x1_bytes_per_utt(arch: str, F: int, T: int, m: int = 32) -> float:
     return total
 
 
+def resnet_tail_launches(arch: str, F: int, T: int, m: int = 32) -> dict:
+    """Per stage L<n>: the bottleneck-tail launches of one utterance-chunk forward
+    (model_impl.h forward_resnet, option res_tail 1): every stride-1 block with 32 / 64 /
+    128 planes runs conv2 + conv3 + residual (+ the next block's conv1 when the next block
+    of the stage is a stride-1 block too: tail2_kernel) in one launch.  Returns
+    {stage: (positions per utterance, planes, fused launches, unfused launches)}."""
+    kind, nblocks = RESNET_ARCHS[arch]
+    out, fi, ti = {}, F, T
+    for li, n in enumerate(nblocks):
+        p = m << li
+        s = 2 if li > 0 else 1
+        fo, to = (fi - 1) // s + 1, (ti - 1) // s + 1
+        if kind == "bottleneck" and p <= 128:
+            tails = [bi for bi in range(n) if not (li > 0 and bi == 0)]
+            fused = sum(1 for bi in tails if bi + 1 < n)
+            out[f"L{li + 1}"] = (fo * to, p, fused, len(tails) - fused)
+        fi, ti = fo, to
+    return out
+
+
 def resnet_model_bytes_per_utt(arch: str, F: int, T: int, m: int = 32) -> float:
     """Algorithmic HBM bytes of one whole bottleneck-ResNet forward (resnet.py:110-260):
     every conv's fp32 input read once and output written once (the stem, the 1x1
@@ -209,6 +229,10 @@ def parse():
                     help="extra model option (wsp_model_set_option), e.g. res2_variant=1; repeatable")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel event timing pass")
     ap.add_argument("--no-f32", action="store_true", help="skip the exact-f32 (precision 0) side measurement")
+    ap.add_argument("--no-kernel-roofline", action="store_true",
+                    help="skip the streams=1 side pass behind the C3 / C4 dominant-kernel roofline")
+    ap.add_argument("--no-hubert-b64", dest="hubert_small_batch", action="store_false",
+                    help="skip the C4 side measurement at the survey's per-rank batch 64")
     ap.add_argument("--sustain-seconds", type=float, default=2.0,
                     help="extra untimed-for-value window reported as value_sustained (>= this many seconds)")
     ap.add_argument("--configs", default="C3,C4",
@@ -550,6 +574,145 @@ def roofline_resnet_model(args, w, kernels, el, steps, streams):
     return roof
 
 
+def standalone_pass(w, handle, tags, steps: int = 2) -> dict:
+    """Per-launch durations of `tags` with the workload on ONE stream (option streams = 1):
+    with the default two utterance-range streams a launch shares the GPU with the other
+    range's kernels, so its event-timed duration is not the kernel's own.  Untimed for
+    `value`; the handle's streams option is restored afterwards."""
+    old = handle.get_option("streams")
+    handle.set_option("streams", 1)
+    try:
+        w["step"]()
+        torch.cuda.synchronize()
+        handle.profile(True)
+        for _ in range(steps):
+            w["step"]()
+        torch.cuda.synchronize()
+        handle.profile(False)
+        out = {}
+        for t in tags:
+            n, ms, fl = handle.profile_query(t)
+            if n:
+                out[t] = {"launches_per_step": n // steps, "avg_ms": ms / n, "flops_per_launch": fl}
+        return out
+    finally:
+        handle.set_option("streams", old)
+
+
+def kernel_roofline_record(name: str, cls: str, launches: int, avg_ms: float, algo_bytes: float, flops: float,
+                           pmc: dict | None, pmc_src: str | None, pmc_algo_bytes: float | None, bound: str) -> dict:
+    """Roofline of ONE kernel from its standalone launch duration: algorithmic bytes and
+    FLOP per launch, fraction of the HBM peak and of the bf16 MFMA peak counted as issued
+    bf16x3 work (3 bf16 MFMAs per fp32 product); PMC traffic (FETCH_SIZE x 2 + WRITE_SIZE,
+    scripts/make_profile_summary.py) of the same kernel's launch in the newest committed
+    profile, with its own algorithmic bytes for the ratio."""
+    gbps = algo_bytes / (avg_ms * 1e-3) / 1e9
+    tf = flops / (avg_ms * 1e-3) / 1e12
+    rec = {"kernel": name, "class": cls, "bound": bound, "launches_per_step": launches,
+           "standalone_avg_ms": round(avg_ms, 4),
+           "algorithmic_bytes_per_launch": algo_bytes, "flops_per_launch": flops,
+           "achieved_gbps": round(gbps, 1), "frac_hbm": round(gbps / HBM_PEAK_GBPS, 4),
+           "achieved_tflops": round(tf, 2), "frac_bf16_peak": round(tf / BF16_MFMA_PEAK_TFLOPS, 4),
+           "frac_issue_peak": round(3 * tf / BF16_MFMA_PEAK_TFLOPS, 4),
+           "traffic": None, "traffic_ratio": None, "traffic_source": pmc_src,
+           "pmc_dur_ms": None, "mfma_util_pmc": None, "clock_ghz_pmc": None}
+    rec["frac"] = rec["frac_hbm"] if bound == "hbm" else rec["frac_issue_peak"]
+    if pmc:
+        ratio = pmc["hbm_bytes"] / pmc_algo_bytes if pmc_algo_bytes else None
+        rec.update({"traffic": round(ratio * algo_bytes) if ratio else pmc["hbm_bytes"],
+                    "traffic_ratio": round(ratio, 4) if ratio else None,
+                    "pmc_dur_ms": round(pmc["pmc_dur_ns"] * 1e-6, 4) if pmc.get("pmc_dur_ns") else None,
+                    "mfma_util_pmc": round(pmc["mfma_util"], 4) if pmc.get("mfma_util") is not None else None,
+                    "clock_ghz_pmc": round(pmc["clock_ghz"], 3) if pmc.get("clock_ghz") else None})
+    return rec
+
+
+def pmc_lookup(pred):
+    """Newest committed PMC record (profiles/r*_<PROFILE_TAG>_traffic.json) whose
+    (symbol, grid) satisfies pred; returns (record, source, grid)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{PROFILE_TAG}_traffic.json")),
+                   key=lambda f: os.path.basename(f))
+    for f in reversed(files):
+        d = json.load(open(f))
+        for key, v in d.items():
+            sym, _, g = key.rpartition("|")
+            if v.get("hbm_bytes") and pred(sym, int(g)):
+                return v, os.path.basename(f) + ":" + sym, int(g)
+    return None, None, None
+
+
+def kernel_roofline_resnet(w) -> dict:
+    """C3: the dominant kernel, the stage-3 bottleneck tail + next conv1 (tail2_kernel<128>,
+    resnet.py:72-107; 126 launches per B = 128 step), from a streams = 1 side pass.  Bytes per
+    position: y1 (p) + residual (4p) + out (4p) + the next block's y1 (p) fp32 values; FLOP per
+    position 2 (9p.p + 4p.p + 4p.p)."""
+    arch, B, T, model = w["arch"], w["B"], w["T"], w["model"]
+    tails = resnet_tail_launches(arch, 80, T)
+    if "L3" not in tails:
+        return None
+    sa = standalone_pass(w, model, ["res_tail.L3"])
+    if "res_tail.L3" not in sa:
+        return None
+    pos, p, nf, nu = tails["L3"]
+    bc = B // -(-B // 64) if B > 64 else B  # the model's 2-GiB utterance chunking at T = 498
+    # class time = fused + unfused launches; bytes / flops summed the same way
+    cls_bytes = 4.0 * pos * bc * (nf * 10 * p + nu * 9 * p)
+    cls_launch = nf + nu
+    k = sa["res_tail.L3"]
+    launches = k["launches_per_step"]
+    avg_bytes = cls_bytes / cls_launch
+    fused_bytes = 4.0 * pos * bc * 10 * p
+    fused_flops = 2.0 * pos * bc * (9 * p * p + 4 * p * p + 4 * p * p)
+    f3, t3 = 80, T
+    for _ in range(2):  # the stride-2 first blocks of stages 2 and 3
+        f3, t3 = (f3 - 1) // 2 + 1, (t3 - 1) // 2 + 1
+    grid = bc * (-(-f3 // 2)) * (-(-t3 // 32)) * 256  # tail2<128>: 2 x 32 positions, 256 threads per block
+    pmc, src, _ = pmc_lookup(lambda s, g: "tail2_kernel<128," in s and g == grid)
+    rec = kernel_roofline_record("tail2_kernel<128, 8, 4, 4> (conv3x3_img.hip: conv2 + conv3 + residual + next conv1)",
+                                 "res_tail.L3", launches, k["avg_ms"], avg_bytes, k["flops_per_launch"], pmc, src,
+                                 fused_bytes, "hbm")
+    rec["note"] = (f"class res_tail.L3 = {nf} fused tail2 + {nu} unfused bottleneck_tail launch(es) per "
+                   f"{bc}-utterance chunk; standalone = option streams 1 side pass; traffic_ratio from the PMC-"
+                   f"serialised tail2<128> launch (grid {grid}) against its {fused_bytes / 1e6:.0f} MB algorithmic")
+    return rec
+
+
+def kernel_roofline_hubert(w) -> dict:
+    """C4: the dominant kernel, HuBERT's first strided CNN GEMM (h_cnn.c1: conv k3 s2,
+    512 -> 512, GELU; fairseq ConvFeatureExtractionModel layer 1 under s3prl.py:80-93), from a
+    streams = 1 side pass.  FLOP per output frame 2 . 512 . 1536; bytes: the conv0 output read
+    once + the output written once (fp32)."""
+    fe = w["fe"]
+    sa = standalone_pass(w, fe, ["h_cnn.c1"])
+    if "h_cnn.c1" not in sa:
+        return None
+    k = sa["h_cnn.c1"]
+    N = w["N"]
+    t0 = (N - 10) // 5 + 1
+    t1 = (t0 - 3) // 2 + 1
+    flops = k["flops_per_launch"]
+    utts = flops / (2.0 * t1 * 512 * 1536)  # utterances per launch (the feature extractor's chunk)
+    algo = 4.0 * 512 * (t0 + t1) * utts
+
+    def is_c1(s, g):  # the 16x16x32 256 x 256 GELU tile at a grid of whole 7 999-row utterances
+        if "conv_gemm_x3ILi4ELi2ELi2ELi4ELi0ELb1ELi0ELb0ELb1ELi1ELi16E" not in s:
+            return False
+        blocks = g // 512 // 2
+        nb = round(blocks * 256 / t1)
+        return nb > 0 and -(-nb * t1 // 256) == blocks
+    pmc, src, grid = pmc_lookup(is_c1)
+    pmc_algo = None
+    if pmc:
+        nb = round(grid // 1024 * 256 / t1)
+        pmc_algo = 4.0 * 512 * (t0 + t1) * nb
+    rec = kernel_roofline_record("conv_gemm_x3<4,2,2,4,...,MF=16> (256 x 256 tile, bf16x3 on 16x16x32 MFMAs), h_cnn.c1",
+                                 "h_cnn.c1", k["launches_per_step"], k["avg_ms"], algo, flops, pmc, src, pmc_algo, "mfma")
+    rec["note"] = (f"{utts:.0f} utterances per launch (feature-extractor chunk); standalone = option streams 1 "
+                   "side pass; frac = issued bf16x3 MFMA work over the dense bf16 peak")
+    return rec
+
+
 def roofline_model_mfma(args, w, gf_utt, el, steps):
     """C4: model-level MFMA roofline -- the whole chain's algorithmic FLOP per step
     (HuBERT-base + ECAPA head, 2 x MACs) over the measured step time, against the dense
@@ -679,6 +842,34 @@ def run_workload(args, arch: str, B: int, steps: int, warmup: int, world: int, r
         if roof is not None and streams > 1 and "note" not in roof and not w["resnet_like"] and not w["hubert"]:
             roof["note"] = ("launch durations measured beside the other utterance range's kernels "
                             "(option streams); --opt streams=1 gives the standalone rate")
+    # the dominant kernel's own roofline (standalone launch duration, one stream), untimed
+    kroof = None
+    if not args.no_profile and not args.no_kernel_roofline:
+        if arch.startswith("ResNet"):
+            kroof = kernel_roofline_resnet(w)
+        elif w["hubert"]:
+            kroof = kernel_roofline_hubert(w)
+    # C4 at the per-rank batch SURVEY §8(d) / BASELINE.md §3 quote (64), beside the default 256:
+    # the same model, the first 64 utterances of the batch, timed the same way
+    small = None
+    if w["hubert"] and B > 64 and args.hubert_small_batch:
+        bs = 64
+        fe_, model_ = w["fe"], w["model"]
+        wav_s, feats_s, emb_s = w["wav"][:bs], w["feats"][:bs], w["emb"][:bs]
+
+        def step_s():
+            fe_.extract(wav_s, cmn=True, out=feats_s)
+            model_.embed(feats_s, out=emb_s)
+        for _ in range(warmup):
+            step_s()
+        barrier()
+        t = time.perf_counter()
+        for _ in range(steps):
+            step_s()
+        barrier()
+        e_s = max_over_ranks(time.perf_counter() - t)
+        small = {"batch_per_gpu": bs, "value": round(world * bs * steps / e_s, 2),
+                 "ms_per_step": round(e_s / steps * 1e3, 3), "steps": steps}
     res = {
         "value": round(value, 2),
         "ms_per_step": round(el / steps * 1e3, 3),
@@ -692,6 +883,8 @@ def run_workload(args, arch: str, B: int, steps: int, warmup: int, world: int, r
         "model_tflops": round(value * gf / 1e3, 2),
         "gflop_per_utt": round(gf, 3),
         "roofline": roof,
+        "kernel_roofline": kroof,
+        "value_batch64": small,
         "dominant_class": dominant_class(kernels, streams) if kernels else None,
         "kernels": kernels,
         "value_sustained": sustained,
@@ -759,6 +952,8 @@ def main():
         "model_tflops": r["model_tflops"],
         "gflop_per_utt": r["gflop_per_utt"],
         "roofline": r["roofline"],
+        "kernel_roofline": r["kernel_roofline"],
+        "value_batch64": r["value_batch64"],
         "dominant_class": r["dominant_class"],
         "options": args.opt or None,
         "kernels": r["kernels"],
@@ -777,6 +972,9 @@ def main():
             PROFILE_TAG = name.lower()
             res["configs"][name] = run_workload(args, sarch, sb, args.sub_steps, args.sub_warmup, world, rank, dev,
                                                 dist, headline=False, cpu_seconds=args.sub_cpu_seconds)
+    # compact per-config summary, LAST key of the line (the driver keeps only the tail of
+    # stdout): value, step time, whole-model roofline fraction, dominant-kernel fraction, CPU
+    res["summary"] = summarize(res)
     if dist is not None:
         # untimed: the AS-Norm cohort-statistics all-reduce (dist.allreduce_sums, one fused
         # f64 buffer over RCCL/xGMI, score_norm.py's cohort means) on this run's ranks,
@@ -786,9 +984,33 @@ def main():
         except Exception as e:  # reported, never fatal to the measurement above
             res["rccl_allreduce_check"] = {"ok": False, "error": repr(e)[:300]}
     if rank == 0:
+        summ = res.pop("summary")
+        if "rccl_allreduce_check" in res:
+            summ["rccl_allreduce_ok"] = (res["rccl_allreduce_check"] or {}).get("ok")
+        res["summary"] = summ  # keep it last
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def summarize(res: dict) -> dict:
+    def one(r, roof, kroof, cpu):
+        d = {"value": r.get("value"), "ms_per_step": r.get("ms_per_step"),
+             "roofline_frac": (roof or {}).get("frac"),
+             "kernel_roofline_frac": (kroof or {}).get("frac"),
+             "cpu_baseline": (cpu or {}).get("value")}
+        if (kroof or {}).get("standalone_avg_ms") is not None:
+            d["kernel_ms"] = kroof["standalone_avg_ms"]
+        return d
+    out = {res["config"]["arch"]: one(res, res.get("roofline"), res.get("kernel_roofline"), res.get("cpu_baseline"))}
+    if res.get("value_batch64"):
+        out[res["config"]["arch"]]["value_batch64"] = res["value_batch64"]["value"]
+    for name, r in (res.get("configs") or {}).items():
+        out[name] = one(r, r.get("roofline"), r.get("kernel_roofline"), r.get("cpu_baseline"))
+        if r.get("value_batch64"):
+            out[name]["value_batch64"] = r["value_batch64"]["value"]
+    out["n_gpus"] = res["n_gpus"]
+    return out
 
 
 if __name__ == "__main__":

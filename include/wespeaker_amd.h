@@ -162,8 +162,14 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *                  [W_a, W_b + W_c, W_c], so the last SE block stores only its gated branch
  *                  (default; equal to 0 up to rounding, ~1e-6), 0 = conv_cat on [out2, out3, out4]
  *   "in_planes"    SimAM-ResNet, before the weights: 32 or 64
+ *   "attn_pipe"    HuBERT front end: 1 = the persistent pipelined attention kernel (keys in
+ *                  LDS halves of 128 frames, the next half in flight; default), 0 = one block
+ *                  per (utterance, head, 128-query block); both bf16x3 MFMA
  *   "layer"        HuBERT front end only, before finalize: -1 = weighted sum of all
- *                  hidden states (default), k = hidden state k alone (s3prl.py:84-87) */
+ *                  hidden states (default), k = hidden state k alone (s3prl.py:84-87)
+ * Deprecated (accepted, mapped to the shipped kernels since r3 pruned the others):
+ *   "attn_lds" and "conv1x1_rows" (any value: no effect), "astp_fused" 2 / 3 (= 1),
+ *   "x3_variant" 0 / 1 / 2 / 9 (= 5). */
 int wsp_model_set_option(wsp_model* m, const char* key, int value);
 /* The current value of a runtime option above (the per-architecture default until set). */
 int wsp_model_get_option(const wsp_model* m, const char* key, int* value);

@@ -5,7 +5,8 @@ synthetic data whose EER is realistic (~1 %), through the whole scoring path of
 local/score.sh / score_norm.sh:
 
   HIP:    wav -> wsp_fbank (+CMN) -> ECAPA forward -> mean-vector cosine
-          (wsp_cosine_pairs) -> AS-Norm top-n (wsp_asnorm_stats) -> EER / minDCF
+          (wsp_cosine_pairs, scoring.trials_cosine_score's {:.5f} score file) -> AS-Norm
+          top-n (wsp_asnorm_stats) + combine (scoring.score_norm's {:.5f} file) -> EER / minDCF
   oracle: f64 numpy fbank -> fp32 torch-CPU ECAPA -> numpy cosine / AS-Norm ->
           EER / minDCF (oracle/scoring_ref, pinned by tests/golden/scoring.npz)
 
@@ -58,14 +59,30 @@ def _trials(rng, spk, n_nontarget):
     return ia, ib, lab
 
 
-def _hip_scores(E, C, mean_vec, ia, ib, top_n):
+def _hip_scores(E, C, mean_vec, ia, ib, top_n, lab, tmp_path):
+    """The product's file path of local/score.sh + local/score_norm.sh: embeddings by
+    key, a trials file, scoring.trials_cosine_score (bin/score.py:38-72, `{:.5f}` score
+    file), scoring.score_norm (bin/score_norm.py:54-115: the score file read back, AS-Norm
+    statistics on the GPU, the combine, `{:.5f}` output) -- both files parsed as
+    compute_metrics.py reads them."""
     from wespeaker_hubert_amd import scoring
-    Ed = torch.from_numpy(E).to(DEV)
-    mvd = torch.from_numpy(mean_vec).to(DEV)
-    cos = scoring.cosine_pairs(Ed - mvd, ia, ib)
-    mu, sd = scoring.asnorm_stats(Ed, torch.from_numpy(C).to(DEV), top_n, mean_vec=mvd)
-    c5 = _r5(cos)
-    return c5, _r5(scoring_ref.asnorm(c5, mu[ia], sd[ia], mu[ib], sd[ib]))
+    keys = [f"u{i:05d}" for i in range(len(E))]
+    emb = {k: E[i] for i, k in enumerate(keys)}
+    cohort = {f"spk{i:05d}": C[i] for i in range(len(C))}
+    trial = tmp_path / "trials"
+    with open(trial, "w") as f:
+        for a, b, l in zip(ia, ib, lab):
+            f.write(f"{keys[a]} {keys[b]} {'target' if l else 'nontarget'}\n")
+    score_file, = scoring.trials_cosine_score(emb, [str(trial)], str(tmp_path / "scores"), mean_vec=mean_vec,
+                                              device=DEV)
+    norm_file = str(tmp_path / "trials.asnorm.score")
+    scoring.score_norm("asnorm", top_n, score_file, norm_file, cohort, emb, mean_vec=mean_vec, device=DEV)
+
+    def col(path):
+        rows = [ln.split() for ln in open(path)]
+        assert [r[0] for r in rows] == [keys[a] for a in ia] and [r[1] for r in rows] == [keys[b] for b in ib]
+        return np.array([float(r[2]) for r in rows])
+    return col(score_file), col(norm_file)
 
 
 def _ref_scores(E, C, mean_vec, ia, ib, top_n):
@@ -89,7 +106,7 @@ def _compare(hip, ref, labels, eer_range):
     return out
 
 
-def test_eer_delta_model_level_ecapa():
+def test_eer_delta_model_level_ecapa(tmp_path):
     from wespeaker_hubert_amd.frontend import compute_fbank
     from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
     arch, n_spk, n_utt, N = "ECAPA_TDNN_c512", 40, 8, 32000
@@ -120,12 +137,12 @@ def test_eer_delta_model_level_ecapa():
         mean_vec = Cu.mean(0).astype(np.float32)                  # mean of the cohort set's embeddings
         C = Cu.reshape(100, 2, -1).mean(1).astype(np.float32)     # per-speaker cohort means (vector_mean.py)
         res.append((E, C, mean_vec))
-    hip = _hip_scores(*res[0], ia, ib, 50)
+    hip = _hip_scores(*res[0], ia, ib, 50, lab, tmp_path)
     orc = _ref_scores(*res[1], ia, ib, 50)
     _compare(hip, orc, lab, (1e-3, 0.05))
 
 
-def test_eer_delta_scoring_vox1o_shape():
+def test_eer_delta_scoring_vox1o_shape(tmp_path):
     rng = np.random.default_rng(11)
     n_spk, Ne, Nc, D, n_trials, top_n = 40, 4874, 10000, 192, 37611, 300
     centres = rng.standard_normal((n_spk, D))
@@ -138,6 +155,6 @@ def test_eer_delta_scoring_vox1o_shape():
                            np.flatnonzero(lab == 0)[:n_trials - n_trials // 10]])
     ia, ib, lab = ia[keep], ib[keep], lab[keep]
     assert len(lab) == n_trials
-    hip = _hip_scores(E, C, mean_vec, ia, ib, top_n)
+    hip = _hip_scores(E, C, mean_vec, ia, ib, top_n, lab, tmp_path)
     orc = _ref_scores(E, C, mean_vec, ia, ib, top_n)
     _compare(hip, orc, lab, (1e-3, 0.05))

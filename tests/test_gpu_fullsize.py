@@ -35,7 +35,7 @@ def _assert_emb(got, ref):
     assert cos.min() >= EMB_COS, cos.min()
 
 
-def test_c5_asnorm_vox1o_shape():
+def test_c5_asnorm_vox1o_shape(tmp_path):
     from wespeaker_hubert_amd import scoring
     rng = np.random.default_rng(55)
     Ne, Nc, D, top_n, n_trials = 4874, 10000, 192, 300, 37611
@@ -61,10 +61,29 @@ def test_c5_asnorm_vox1o_shape():
     np.testing.assert_allclose(s, ref_s, atol=1e-12)
     s5 = np.array([float(f"{v:.5f}") for v in s])
     r5 = np.array([float(f"{v:.5f}") for v in ref_s])
-    got = scoring_ref.asnorm(s5, mu[ia], sd[ia], mu[ib], sd[ib])
     ref = scoring_ref.asnorm(r5, rmu[ia], rsd[ia], rmu[ib], rsd[ib])
+    # the product's score files: bin/score.py's `{:.5f}` trial scores, then bin/score_norm.py's
+    # read-back + AS-Norm combine + `{:.5f}` output (scoring.trials_cosine_score / score_norm)
+    keys = [f"id{i:05d}" for i in range(Ne)]
+    emb = {k: E[i] for i, k in enumerate(keys)}
+    trial = tmp_path / "vox1_O_cleaned.kaldi"
+    with open(trial, "w") as f:
+        for a, b in zip(ia, ib):
+            f.write(f"{keys[a]} {keys[b]} {'target' if a % 7 == b % 7 else 'nontarget'}\n")
+    score_file, = scoring.trials_cosine_score(emb, [str(trial)], str(tmp_path / "scores"), mean_vec=mean_vec,
+                                              device=DEV)
+    norm_file = str(tmp_path / "vox1_O_cleaned.kaldi.asnorm.score")
+    scoring.score_norm("asnorm", top_n, score_file, norm_file, {f"spk{i}": C[i] for i in range(Nc)}, emb,
+                       mean_vec=mean_vec, device=DEV)
+    rows = [ln.split() for ln in open(norm_file)]
+    assert len(rows) == n_trials and all(len(r) == 8 for r in rows)
+    got = np.array([float(r[2]) for r in rows])
     assert np.abs(got - ref).max() < 1e-3  # AS-Norm scores, written {:.5f} by the reference
-    assert np.mean(np.abs(got - ref) < 1e-5) > 0.999
+    assert np.mean(np.abs(got - ref) < 1.5e-5) > 0.999
+    # side columns (score_norm.py:111-115): |e - mean|, |t - mean|, mu_e, mu_t at 4 decimals
+    e_mag = np.linalg.norm(Em64, axis=1)
+    np.testing.assert_allclose([float(r[4]) for r in rows], e_mag[ia], atol=6e-5)
+    np.testing.assert_allclose([float(r[7]) for r in rows], rmu[ib], atol=6e-5)
 
 
 def test_asnorm_top_n_larger_than_cohort_uses_whole_cohort():

@@ -187,3 +187,36 @@ def test_lds_attention_ragged_long_utterances(sd_np):
     for i, w in enumerate(wavs):
         one = fe.extract(torch.from_numpy(w[None]).to(DEV), cmn=True)[0]
         np.testing.assert_allclose(feats[offs[i]:offs[i + 1]].cpu().numpy(), one.cpu().numpy(), atol=1e-5, rtol=0)
+
+
+def test_c4_bench_shape_rows_match_oracle(sd_np, sd_t):
+    """C4 at the bench shape: B = 256 x 5 s with the default front-end options (two
+    utterance-range streams of 128, each split into 57 / 57 / 14-utterance feature-
+    extractor chunks: the 2-GiB conv0 operand cap) -> CMN -> ECAPA_TDNN_GLOB_c512(768).
+    Rows at the start, at both chunk boundaries and the stream boundary, and at the end
+    equal their batch-of-one embeddings and the oracle chain at the north-star bar."""
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    B, W = 256, 80000
+    rows = (0, 56, 57, 127, 128, 255)
+    wav = _wav(13, B, W)
+    fe = _frontend(sd_np)
+    assert fe.get_option("streams") == 2
+    m = HipSpeakerModel("ECAPA_TDNN_GLOB_c512", feat_dim=768, embed_dim=192)
+    sd_e = synth_state_dict(12, m.state_dict_layout())
+    m.load_state_dict(sd_e)
+    m.to(DEV)
+    wd = torch.from_numpy(wav).to(DEV)
+    got = m(fe.extract(wd, cmn=True))[-1].cpu().numpy()
+    assert got.shape == (B, 192) and np.all(np.isfinite(got))
+    for r in rows:
+        one = m(fe.extract(wd[r:r + 1].contiguous(), cmn=True))[-1].cpu().numpy()[0]
+        assert np.abs(got[r] - one).max() <= 1e-6, (r, np.abs(got[r] - one).max())
+    with torch.no_grad():
+        f_ref = _cmn(hubert_ref.s3prl_frontend(torch.from_numpy(wav[list(rows)]), sd_t))
+        ref = models_ref.forward("ECAPA_TDNN_GLOB_c512", f_ref,
+                                 {k: torch.from_numpy(v) for k, v in sd_e.items()})[-1].numpy()
+    g = got[list(rows)]
+    d = np.abs(g - ref).max()
+    cos = (g * ref).sum(1) / (np.linalg.norm(g, axis=1) * np.linalg.norm(ref, axis=1))
+    assert d < EMB_ATOL, f"max |delta| {d}"
+    assert cos.min() >= EMB_COS

@@ -269,7 +269,8 @@ def test_group_means():
 SEG_FRAMES = [3, 77, 498, 150, 2, 263, 41]
 
 
-@pytest.mark.parametrize("prec", [(1, 4), (1, 5), (0, 5)], ids=["bf16x3_256swz", "bf16x3_256sq", "f32"])
+@pytest.mark.parametrize("prec", [(1, 4), (1, 5), (1, 6), (0, 5)],
+                         ids=["bf16x3_256swz", "bf16x3_256sq", "bf16x3_256sq_mf16", "f32"])
 @pytest.mark.parametrize("arch", ["ECAPA_TDNN_GLOB_c512", "ECAPA_TDNN_c1024"])
 def test_ecapa_segmented_batch_equals_batch_of_one(arch, prec):
     """Ragged batch (wsp_model_forward_segments): utterances of 2..498 frames in one

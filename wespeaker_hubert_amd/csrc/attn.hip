@@ -425,12 +425,7 @@ void launch_attn(const float* qkv, int ldq, float* out, int ldo, int B, int T, i
   WSP_CHECK(dh == kDh, "attn: head dim must be 64");
   WSP_CHECK(B > 0 && T > 0 && H > 0 && ldq >= 3 * H * dh && ldq % 4 == 0 && ldo % 4 == 0, "attn: bad shape");
   if (pipe) {
-    static int ncu = 0;
-    if (!ncu) {
-      int dev = 0;
-      WSP_HIP(hipGetDevice(&dev));
-      WSP_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
+    const int ncu = device_cu_count();
     const int nqb = (T + kQB - 1) / kQB;  // segmented: T = longest utterance
     const int nitems = B * H * nqb;
     hipLaunchKernelGGL(attn_pipe_kernel, dim3(std::min(nitems, ncu)), dim3(512), kLdsPipe, s, qkv, ldq, out, ldo, T,

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <string>
 
@@ -73,6 +74,27 @@ __device__ __forceinline__ float gelu_as(float y) {
 }
 
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+// CU count of the CURRENT device, cached per device id (launch geometry of the
+// persistent / strip kernels).  Concurrent first calls from several host threads
+// store the same value, so a relaxed atomic per device is enough.
+inline int device_cu_count() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  WSP_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) {
+    int n = 0;
+    WSP_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    return n > 0 ? n : 256;
+  }
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
+    WSP_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    if (n <= 0) n = 256;
+    cache[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
+}
 
 // Utterance of row m in a segmented (ragged) batch: seg[b] <= m < seg[b+1],
 // seg = int32 [nseg+1] row offsets (binary search; seg is tiny and cache-hot).

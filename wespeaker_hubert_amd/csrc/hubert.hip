@@ -43,7 +43,11 @@ __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restr
   const int b = blockIdx.y, t0 = blockIdx.x * kMT, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int N = wseg ? wseg[b + 1] - wseg[b] : N_;
   const int T0 = oseg ? oseg[b + 1] - oseg[b] : T0_;
-  if (t0 >= T0) return;  // block-uniform: past this utterance
+  double* part = mom + ((size_t)b * gridDim.x + blockIdx.x) * kNM;  // this block's partial moments
+  if (t0 >= T0) {  // block-uniform: past this utterance (ragged batch); its partials are zero
+    if (tid < kNM) part[tid] = 0.0;
+    return;
+  }
   const float* x = wav + (wseg ? (size_t)wseg[b] : (size_t)b * ldw);
   for (int i = tid; i < kMT * kS0 + kK0; i += 256) {
     const int n = t0 * kS0 + i;
@@ -66,8 +70,8 @@ __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restr
       for (int k = j; k < kK0; ++k, ++q) m[q] = fma(v[j], v[k], m[q]);
     }
   }
-  // fixed-order reduction: lanes (butterfly), waves (LDS), then one f64 atomic per
-  // moment and block (block order varies: the sums are exact to ~1e-16 relative)
+  // fixed-order reduction: lanes (butterfly), waves (LDS), then one partial per moment and
+  // block, summed in block order by conv0_kernel (deterministic: no atomics)
 #pragma unroll
   for (int i = 0; i < kNM; ++i) {
     double v = m[i];
@@ -76,7 +80,7 @@ __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restr
     if (lane == 0) red[wave][i] = v;
   }
   __syncthreads();
-  if (tid < kNM) atomicAdd(&mom[(size_t)b * kNM + tid], red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]);
+  if (tid < kNM) part[tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
 }
 
 // out = GELU(GroupNorm(y)).  One thread per channel, one block per (128-frame chunk,
@@ -86,9 +90,10 @@ __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restr
 __global__ __launch_bounds__(kC0) void conv0_kernel(const float* __restrict__ wav, int N_, int ldw, int T0_,
                                                     const float* __restrict__ w, const float* __restrict__ gamma,
                                                     const float* __restrict__ beta, const double* __restrict__ mom,
-                                                    float* __restrict__ out, const int* __restrict__ wseg,
+                                                    int nmb, float* __restrict__ out, const int* __restrict__ wseg,
                                                     const int* __restrict__ oseg) {
   __shared__ float xs[kTC * kS0 + kK0];
+  __shared__ double ms[kNM];
   const int b = blockIdx.y, t0 = blockIdx.x * kTC, c = threadIdx.x;
   const int N = wseg ? wseg[b + 1] - wseg[b] : N_;
   const int T0 = oseg ? oseg[b + 1] - oseg[b] : T0_;
@@ -99,14 +104,22 @@ __global__ __launch_bounds__(kC0) void conv0_kernel(const float* __restrict__ wa
     const int n = t0 * kS0 + i;
     xs[i] = n < N ? x[n] : 0.f;
   }
+  // the utterance's waveform moments: its moments blocks' partials summed in block order
+  if (c < kNM) {
+    const double* pm = mom + (size_t)b * nmb * kNM + c;
+    double a = 0.0;
+    for (int i = 0; i < (T0 + kMT - 1) / kMT; ++i) a += pm[(size_t)i * kNM];
+    ms[c] = a;
+  }
   float wr[kK0];
 #pragma unroll
   for (int k = 0; k < kK0; ++k) wr[k] = w[c * kK0 + k];
+  __syncthreads();
   // this channel's first and second moments from the utterance's waveform moments (f64;
   // var = E[y^2] - mean^2 is exact enough in f64 for fp32 outputs)
   float scale, shift;
   {
-    const double* mo = mom + (size_t)b * kNM;
+    const double* mo = ms;
     double s0 = 0.0, s1 = 0.0;
     int q = kK0;
 #pragma unroll
@@ -248,13 +261,15 @@ void launch_hubert_conv0(const float* wav, int B, int N, int ldw, int T0, const 
     WSP_CHECK(ldw >= N, "hubert conv0: ldw < N");
   }
   WSP_CHECK(B > 0 && T0 > 0, "hubert conv0: empty batch");  // segmented: T0 = longest utterance's frames
-  WSP_HIP(hipMemsetAsync(stats, 0, sizeof(double) * kNM * B, s));  // kNM <= 2 * kC0 doubles per utterance
-  hipLaunchKernelGGL(conv0_moments_kernel, dim3((T0 + kMT - 1) / kMT, B), dim3(256), 0, s, wav, N, ldw, T0, stats,
-                     wseg, oseg);
+  // stats: hubert_conv0_stats_doubles(B, T0) partial moments, one set per (utterance, moments block)
+  const int nmb = (T0 + kMT - 1) / kMT;
+  hipLaunchKernelGGL(conv0_moments_kernel, dim3(nmb, B), dim3(256), 0, s, wav, N, ldw, T0, stats, wseg, oseg);
   hipLaunchKernelGGL(conv0_kernel, dim3((T0 + kTC - 1) / kTC, B), dim3(kC0), 0, s, wav, N, ldw, T0, w, gamma, beta,
-                     stats, out, wseg, oseg);
+                     stats, nmb, out, wseg, oseg);
   WSP_HIP(hipGetLastError());
 }
+
+size_t hubert_conv0_stats_doubles(int B, int T0) { return (size_t)B * ((T0 + kMT - 1) / kMT) * kNM; }
 
 void launch_layernorm(const LayerNormArgs& p, hipStream_t s) {
   WSP_CHECK(p.M > 0 && (p.D == 512 || p.D == 768), "layernorm: D must be 512 or 768");

@@ -204,6 +204,7 @@ HubertPlan Model::Impl::hubert_plan(int B, const int* lens) const {
     pl.maxA = std::max(pl.maxA, c.rows[0]);
     pl.maxB = std::max(pl.maxB, c.rows[1]);
     pl.maxChunk = std::max(pl.maxChunk, c.b1 - c.b0);
+    pl.maxStats = std::max(pl.maxStats, hubert_conv0_stats_doubles(c.b1 - c.b0, c.maxT0));
   }
   pl.maxT6 = *std::max_element(T[6].begin(), T[6].end());
   WSP_CHECK(pl.M * kFfn * sizeof(float) < ((size_t)1 << 31) - 64,
@@ -213,7 +214,7 @@ HubertPlan Model::Impl::hubert_plan(int B, const int* lens) const {
 
 size_t Model::Impl::hubert_ws_floats(const HubertPlan& pl, size_t* offs) const {
   const size_t M = pl.M;
-  const size_t sizes[] = {pl.maxA * kConvDim, pl.maxB * kConvDim, (size_t)4 * pl.maxChunk * kConvDim,  // cnnA, cnnB, stats
+  const size_t sizes[] = {pl.maxA * kConvDim, pl.maxB * kConvDim, 2 * pl.maxStats,  // cnnA, cnnB, stats (f64)
                           M * kHidden,        M * kHidden,        M * 3 * kHidden,                     // x, x1, qkv
                           M * kHidden,        M * kFfn,                                                // ao, ffn / pos
                           pl.offs.size()};                                                             // int32 offsets

@@ -163,6 +163,8 @@ void launch_fbank(const void* wav, int dtype, int B, int N, int ld, float scale,
 void launch_hubert_conv0(const float* wav, int B, int N, int ldw, int T0, const float* w, const float* gamma,
                          const float* beta, double* stats, float* out, hipStream_t s, const int* wseg = nullptr,
                          const int* oseg = nullptr);
+// doubles of launch_hubert_conv0's `stats` scratch for B utterances of at most T0 conv0 frames
+size_t hubert_conv0_stats_doubles(int B, int T0);
 // out[row] = LayerNorm(x[row] (+ add[row][remap(c)])) with remap(c) = (c/gin)*gout + c%gin;
 // if feat: feat[b][t'] (=|+=) feat_w * out[row] for t' = t, and t' in [T, Tout) when t = T-1.
 struct LayerNormArgs {

@@ -244,8 +244,8 @@ void Model::set_option(const std::string& key, int value) {
     WSP_CHECK(value == 0 || value == 1, "attn_pipe must be 0 or 1");
     impl->attn_pipe = value;
   } else if (key == "astp_fused") {
-    WSP_CHECK(value == 0 || value == 1, "astp_fused must be 0 (linear2 GEMM + pooling kernel) or 1 (fused)");
-    impl->astp_fused_on = value;
+    WSP_CHECK(value >= 0 && value <= 3, "astp_fused must be 0 (linear2 GEMM + pooling kernel) or 1 (fused)");
+    impl->astp_fused_on = value ? 1 : 0;  // 2 / 3: former fused variants (r3 pruned), deprecated aliases of 1
   } else if (key == "conv3x3_img") {
     WSP_CHECK(value >= 0 && value <= 3, "conv3x3_img must be 0 (off), 1 (32 / 64 channels) or 2 / 3 (also 128)");
     impl->conv3x3_img_on = value;
@@ -258,8 +258,11 @@ void Model::set_option(const std::string& key, int value) {
               "or 4 (halo-free strips, c1024 widths; else as 3)");
     impl->res2_variant = value;
   } else if (key == "x3_variant") {
-    WSP_CHECK(value >= 3 && value <= 6, "x3_variant must be 3, 4, 5 or 6 (5 on 16x16x32 MFMAs)");
-    impl->x3_variant = value;
+    WSP_CHECK((value >= 0 && value <= 6) || value == 9, "x3_variant must be 3, 4, 5 or 6 (5 on 16x16x32 MFMAs)");
+    // 0 / 1 (unswizzled tiles), 2 / 9 (LDS-DMA tiles): pruned in r3, deprecated aliases of 5
+    impl->x3_variant = value >= 3 && value <= 6 ? value : 5;
+  } else if (key == "attn_lds" || key == "conv1x1_rows") {
+    // pruned in r3 (hubert.hip's streaming mha_kernel, conv1x1_rows.hip): accepted, no effect
   } else {
     throw InvalidArg{"unknown option " + key};
   }

@@ -96,6 +96,7 @@ struct HubertPlan {
   int B = 0;
   size_t M = 0, Mout = 0, maxA = 0, maxB = 0;
   int maxChunk = 0, maxT6 = 0;
+  size_t maxStats = 0;  // doubles of conv0 partial moments (hubert_conv0_stats_doubles) of the largest chunk
   std::vector<HubertChunk> chunks;
   std::vector<int> offs;
 };

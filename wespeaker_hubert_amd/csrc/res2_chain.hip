@@ -629,19 +629,8 @@ void launch_res2_chain(const Res2Args& p, int w, hipStream_t s) {
 
 // Strips (variant 4, W = 128): one round of two blocks per CU over the batch's rows,
 // at least 64 rows per strip (the 12d warm-up / drain rows are per strip).
-static int device_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    WSP_HIP(hipGetDevice(&dev));
-    WSP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    if (cus <= 0) cus = 256;
-  }
-  return cus;
-}
-
 int res2_chain_rout(int dil, int variant, int M) {
-  if (variant == 4) return std::max(64, ceil_div(M, 2 * device_cus()));
+  if (variant == 4) return std::max(64, ceil_div(M, 2 * device_cu_count()));
   return res2_rows(variant) - 12 * dil;
 }
 
