@@ -55,10 +55,11 @@ def _hip_model(arch, seed, precision=1, variant=5, **kw):
     return m.to(DEV), sd
 
 
-# the shipped bf16x3 tile families (x3_variant 5 = 256x256 ECAPA / HuBERT default, 6 = the same tile
-# on 16x16x32 MFMAs, 4 = 256x128 ResNet default, 3 = 128x128) and the exact-f32 kernels (precision 0)
-PREC = [(1, 5), (1, 6), (1, 4), (1, 3), (0, 5)]
-PREC_IDS = ["bf16x3_256sq", "bf16x3_256mf16", "bf16x3_256swz", "bf16x3_128swz", "f32"]
+# the shipped bf16x3 tile families (x3_variant 5 = 256x256, 6 = the same tile on 16x16x32 MFMAs,
+# 7 = 6 staged by LDS-DMA (ECAPA / HuBERT default), 4 = 256x128 ResNet default, 3 = 128x128) and
+# the exact-f32 kernels (precision 0)
+PREC = [(1, 5), (1, 6), (1, 7), (1, 4), (1, 3), (0, 5)]
+PREC_IDS = ["bf16x3_256sq", "bf16x3_256mf16", "bf16x3_256dma", "bf16x3_256swz", "bf16x3_128swz", "f32"]
 
 
 @pytest.mark.parametrize("prec", PREC, ids=PREC_IDS)
@@ -269,8 +270,8 @@ def test_group_means():
 SEG_FRAMES = [3, 77, 498, 150, 2, 263, 41]
 
 
-@pytest.mark.parametrize("prec", [(1, 4), (1, 5), (1, 6), (0, 5)],
-                         ids=["bf16x3_256swz", "bf16x3_256sq", "bf16x3_256sq_mf16", "f32"])
+@pytest.mark.parametrize("prec", [(1, 4), (1, 5), (1, 6), (1, 7), (0, 5)],
+                         ids=["bf16x3_256swz", "bf16x3_256sq", "bf16x3_256sq_mf16", "bf16x3_256dma", "f32"])
 @pytest.mark.parametrize("arch", ["ECAPA_TDNN_GLOB_c512", "ECAPA_TDNN_c1024"])
 def test_ecapa_segmented_batch_equals_batch_of_one(arch, prec):
     """Ragged batch (wsp_model_forward_segments): utterances of 2..498 frames in one
@@ -300,3 +301,23 @@ def test_fbank_segments_equal_per_utterance():
     for i, w in enumerate(wavs):
         one = compute_fbank(torch.from_numpy(w[None]).to(DEV), cmn=True)[0]
         assert torch.equal(feats[off[i]:off[i + 1]], one), i
+
+
+@pytest.mark.parametrize("arch,B,T", [("ECAPA_TDNN_c1024", 5, 498), ("ECAPA_TDNN_GLOB_c512", 3, 301),
+                                      ("ECAPA_TDNN_c512", 2, 40)])
+def test_lds_dma_tile_bit_identical_to_register_staged(arch, B, T):
+    """x3_variant 7 (conv_gemm_x3_t6.hip: every operand by LDS-DMA, the fp32 A split at fragment
+    time) multiplies the same bf16 hi / lo products in the same MFMA order as 6: the embeddings
+    are equal bit for bit, uniform and ragged."""
+    x = synth_feats(123, B, T, 80)
+    outs = []
+    for v in (6, 7):
+        m, _ = _hip_model(arch, 31, 1, v, feat_dim=80, embed_dim=192)
+        _, e = m(torch.from_numpy(x).to(DEV))
+        frames = [T, max(2, T // 3), T - 1][:B] if B <= 3 else [T] * B
+        feats = np.concatenate([x[i, :f] for i, f in enumerate(frames)])
+        off = torch.tensor(np.concatenate([[0], np.cumsum(frames)]), dtype=torch.int32, device=DEV)
+        es = m.embed_segments(torch.from_numpy(feats).to(DEV), off)
+        outs.append((e.cpu().numpy(), es.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])

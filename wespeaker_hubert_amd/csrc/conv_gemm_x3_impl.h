@@ -360,6 +360,8 @@ void t_2x2_2x2_sw(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t
 void t_4x2_2x2_sw(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);   // 256 x 128 swizzled (v4)
 void t_4x2_2x4_sw1(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);  // 256 x 256, one set (v5)
 void t_4x2_2x4_mf16(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);  // v5 on 16x16x32 (v6)
+bool g256_supported(const ConvGemmArgs&);                                              // v7 operands
+void t_g256(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);         // v6 by LDS-DMA (v7)
 }  // namespace x3
 
 }  // namespace wsp

@@ -44,7 +44,7 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
   if (arch == "ECAPA_TDNN_c512" || arch == "ECAPA_TDNN_GLOB_c512" || arch == "ECAPA_TDNN_c1024" ||
       arch == "ECAPA_TDNN_GLOB_c1024") {
     m.ecapa = true;
-    m.x3_variant = 6;  // the 256 x 256 tile on 16x16x32 MFMAs: C2 +0.8-1.2 % over 5 (r3)
+    m.x3_variant = 7;  // 6 (the 256 x 256 tile on 16x16x32 MFMAs, r3) with LDS-DMA staging (r4)
     m.C = (arch.find("c1024") != std::string::npos) ? 1024 : 512;
     m.glob = arch.find("GLOB") != std::string::npos;
     WSP_CHECK(feat_dim > 0 && feat_dim % 4 == 0, "ECAPA feat_dim must be a positive multiple of 4");
@@ -89,6 +89,7 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
     m.ecapa = false;
     m.hubert = true;
     m.feat_dim = 1;
+    m.x3_variant = 7;  // every GEMM whose operands family 7 takes (r4), the rest on 6
     m.streams = 2;  // HuBERT + ECAPA C4 chain +2.6 %
     m.build_hubert_params();
   } else {
@@ -258,9 +259,10 @@ void Model::set_option(const std::string& key, int value) {
               "or 4 (halo-free strips, c1024 widths; else as 3)");
     impl->res2_variant = value;
   } else if (key == "x3_variant") {
-    WSP_CHECK((value >= 0 && value <= 6) || value == 9, "x3_variant must be 3, 4, 5 or 6 (5 on 16x16x32 MFMAs)");
-    // 0 / 1 (unswizzled tiles), 2 / 9 (LDS-DMA tiles): pruned in r3, deprecated aliases of 5
-    impl->x3_variant = value >= 3 && value <= 6 ? value : 5;
+    WSP_CHECK((value >= 0 && value <= 7) || value == 9,
+              "x3_variant must be 3, 4, 5, 6 (5 on 16x16x32 MFMAs) or 7 (6 staged by LDS-DMA)");
+    // 0 / 1 (unswizzled tiles), 2 / 9 (the r2 LDS-DMA tiles): pruned in r3, deprecated aliases of 5
+    impl->x3_variant = value >= 3 && value <= 7 ? value : 5;
   } else if (key == "attn_lds" || key == "conv1x1_rows") {
     // pruned in r3 (hubert.hip's streaming mha_kernel, conv1x1_rows.hip): accepted, no effect
   } else {
