@@ -2,7 +2,8 @@
 // not part of the product).  Plain GEMM shapes (taps = 1) or 1-D convs:
 //   gemm_bench M N K [taps [reps]] ...   (K = cin * taps)
 // For every kernel variant: average launch time over `reps` launches with HIP
-// events, algorithmic TFLOP/s (2*M*N*K), and max |diff| against variant 4.
+// events, algorithmic TFLOP/s (2*M*N*K), and max |diff| against variant 4
+// (r4: families 6 and 7 in interleaved rounds).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -96,7 +97,8 @@ int main(int argc, char** argv) {
     struct V {
       const char* name;
       int kind;
-    } vars[] = {{"x3_256swz", 4}, {"x3_128swz", 3}, {"x3_256sq", 5}, {"f32", -1}};
+    } vars[] = {{"x3_256swz", 4}, {"x3_256mf16", 6}, {"x3_256dma", 7}, {"x3_256mf16", 6}, {"x3_256dma", 7},
+                {"x3_256mf16", 6}, {"x3_256dma", 7}};
     std::vector<float> ref((size_t)M * N), out((size_t)M * N);
     for (auto& v : vars) {
       ConvGemmArgs q = g;

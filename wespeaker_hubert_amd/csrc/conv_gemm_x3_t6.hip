@@ -11,8 +11,12 @@
 // ends with one vmcnt(0) + barrier and the next DMAs are issued right behind it.  The split
 // moves to the fragment reads (8 floats -> bf16x8 hi + lo per 16x16x32 A fragment), where its
 // VALU issues beside the MFMAs.  Same products, same MFMA order, same epilogue as family 6:
-// bit-identical results (tools/gemm_g3.hip: C x C 0.750 -> 0.640 ms, conv_cat 3.14 -> 2.70 ms
-// standalone).
+// bit-identical results.  The k-loop alone (timing build without epilogue) runs 0.56-0.58 ms on
+// the C x C shape against 0.64-0.66 with plain stores and 0.69-0.72 for family 6 with the bias +
+// ReLU epilogue (tools/g7_check.hip); in the model (C2, r4) conv_cat 2.72-2.78 -> 2.69-2.70 ms,
+// C2 +0.9 %.  The epilogue (the 0.5 GB C write at one block per CU, nothing overlapping it) is
+// ~15-25 % of a block at K <= 1024; a persistent form fetching the next tile's first k-tiles
+// behind it measured no faster (profiles/r4e_gemm_family7_experiments.txt).
 //
 // LDS per stage (64 KB; two stages = 128 KB, one block of 8 waves per CU):
 //   A [256 rows][32 k] fp32, 16-B chunk c of row r at slot c ^ ((r >> 1) & 5) — the two
@@ -23,7 +27,8 @@
 // chunk it fetches (cdna_hip_programming.md §5.4 rule 21).
 // Supported operands: 1-D convs with one or three concatenated A segments on 32-aligned k-tiles
 // (taps / dilation / padding / stride / ragged batches as ALoader), no added operand, no
-// grouped columns, N % 256 == 0 — launch_conv_gemm_x3 routes everything else to family 6.
+// grouped columns, N % 256 == 0, and an epilogue without SE column sums or residual —
+// launch_conv_gemm_x3 routes everything else to family 6.
 #include "conv_gemm_x3_impl.h"
 
 namespace wsp {
@@ -38,6 +43,9 @@ __device__ __forceinline__ void g_dma(__amdgpu_buffer_rsrc_t r, unsigned char* l
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, 0, 0, 0);
 }
 
+// DENSE: 1x1 row-local GEMMs (taps 1, no padding, stride 1: A row = output row, also in ragged
+// batches) keep one register per A row; the conv form keeps ALoader's (row, frame, length) triple.
+template <bool DENSE>
 __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, const __bf16* __restrict__ whi,
                                                       const __bf16* __restrict__ wlo) {
   using L = Lds<true, 16>;
@@ -55,13 +63,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
 
   // ---- A rows of this lane: DMA i (0..3) of wave w fills LDS rows (4 w + i) * 8 .. + 7, lane
   // l row + (l >> 3), slot l & 7 <- source chunk (l & 7) ^ swizzle(row) (ALoader's row logic)
-  int a_r[4], a_t[4], a_l[4], a_c[4];
+  // row = 32 w + 8 i + (l >> 3): swizzle(row) = (row >> 1) & 5 = ((l >> 4) & 1) | ((i & 1) << 2)
+  const int ac0 = 4 * ((lane & 7) ^ ((lane >> 4) & 1)), ac1 = ac0 ^ 16;
+  int a_r[4], a_t[DENSE ? 1 : 4], a_l[DENSE ? 1 : 4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int row = (4 * wave + i) * 8 + (lane >> 3);
-    a_c[i] = 4 * ((lane & 7) ^ ((row >> 1) & 5));
-    const int m = m0 + row;
-    if (p.seg) {
+    const int m = m0 + (4 * wave + i) * 8 + (lane >> 3);
+    if constexpr (DENSE) {
+      a_r[i] = m < p.M ? m : -1;
+    } else if (p.seg) {
       const int mm = m < p.M ? m : p.M - 1;
       const int b = seg_of(p.seg, p.nseg, mm);
       const int t = (mm - p.seg[b]) * p.stride;
@@ -87,6 +97,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
   }
   const __amdgpu_buffer_rsrc_t rwh = make_rsrc(whi);
   const __amdgpu_buffer_rsrc_t rwl = make_rsrc(wlo);
+  const int nk = p.Kp / BK;  // >= 2 (Kp % 64 == 0)
   int jt = 0, ct = 0;  // tap and channel of the next k-tile to fetch (k-tiles are fetched in order)
   auto dma = [&](int kt, int buf) {
     unsigned char* st = smem + buf * kGStage;
@@ -105,9 +116,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
     const __amdgpu_buffer_rsrc_t ra = make_rsrc(base);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int tt = a_t[i] + off;
-      const bool ok = tt >= 0 && tt < a_l[i];
-      g_dma(ra, st + (4 * wave + i) * 1024, ok ? ((a_r[i] + off) * ld + cl + a_c[i]) * 4 : kOOB);
+      if constexpr (DENSE) {
+        g_dma(ra, st + (4 * wave + i) * 1024, a_r[i] >= 0 ? (a_r[i] * ld + cl + (i & 1 ? ac1 : ac0)) * 4 : kOOB);
+      } else {
+        const int tt = a_t[i] + off;
+        const bool ok = tt >= 0 && tt < a_l[i];
+        g_dma(ra, st + (4 * wave + i) * 1024, ok ? ((a_r[i] + off) * ld + cl + (i & 1 ? ac1 : ac0)) * 4 : kOOB);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -166,7 +181,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
       }
   };
 
-  const int nk = p.Kp / BK;  // >= 2 (Kp % 64 == 0)
   dma(0, 0);
   dma(1, 1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0 landed (8 DMAs per k-tile and lane)
@@ -199,12 +213,17 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
 namespace x3 {
 
 bool g256_supported(const ConvGemmArgs& p) {
-  return p.N % 256 == 0 && !p.conv2d && !p.gcols && p.amode == kACat && uniform_ktiles(p);
+  // SE column-sum and residual epilogues measured no faster here than on family 6 (r4, in model:
+  // the epilogue, ~15-25 % of a 256 x 256 block at K <= 1024, is the same code) and stay there
+  return !p.colsum && !p.res && p.N % 256 == 0 && !p.conv2d && !p.gcols && p.amode == kACat && uniform_ktiles(p);
 }
 
 void t_g256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s) {
   const int nwg = ((p.M + 255) / 256) * (p.N / 256);
-  hipLaunchKernelGGL(conv_gemm_g, dim3(nwg), dim3(512), 2 * kGStage, s, p, h, l);
+  if (p.taps == 1 && p.pad == 0 && p.stride == 1)
+    hipLaunchKernelGGL(conv_gemm_g<true>, dim3(nwg), dim3(512), 2 * kGStage, s, p, h, l);
+  else
+    hipLaunchKernelGGL(conv_gemm_g<false>, dim3(nwg), dim3(512), 2 * kGStage, s, p, h, l);
   WSP_HIP(hipGetLastError());
 }
 
