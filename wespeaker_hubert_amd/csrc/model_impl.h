@@ -221,7 +221,8 @@ struct Model::Impl {
   // 1 = bf16x3 split MFMA (default), 0 = exact f32 MFMA
   int precision = 1;
   // bf16x3 tile family (conv_gemm_x3.hip): 5 = 256 x 256 where N % 256 == 0, else 256 x 128;
-  // 4 = 256 x 128; 3 = 128 x 128 (option "x3_variant")
+  // 4 = 256 x 128; 3 = 128 x 128; 6 = 5 on 16x16x32 MFMAs; 7 = 6 with plain-epilogue GEMMs
+  // staged by LDS-DMA (conv_gemm_x3_t6.hip) (option "x3_variant")
   int x3_variant = 5;
 
   // concurrent sub-batches (option "streams"): the batch's utterances are split
