@@ -138,10 +138,10 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *   "x3_variant"   bf16x3 conv-GEMM tile family (all with swizzled LDS rows): 3 = 128x128,
  *                  4 = 256x128 (ResNet default), 5 = 256x256 where N % 256 == 0, else 256x128
  *                  (SimAM-ResNet default), 6 = 5 with the 256x256 tile on 16x16x32 MFMAs,
- *                  7 = 6 with the plain-epilogue 1-D GEMMs (no SE column sums, no residual)
- *                  on one LDS-DMA tile kernel (conv_gemm_x3_t6.hip: A fp32 and W hi / lo
- *                  staged by buffer_load ... lds, A split at fragment time; bit-identical to 6;
- *                  ECAPA-TDNN and HuBERT default)
+ *                  7 = 6 with the 1-D GEMMs (N % 256 == 0, one or three concatenated A
+ *                  segments) on one LDS-DMA tile kernel (conv_gemm_x3_t6.hip: A fp32 and
+ *                  W hi / lo staged by buffer_load ... lds, A split at fragment time, outputs
+ *                  through LDS as whole rows; bit-identical to 6; ECAPA-TDNN and HuBERT default)
  *   "res2_fused"   1 = one res2_chain launch per SE_Res2Block (default), 0 = 7 GEMMs
  *   "res2_variant" res2_chain kernel: 128-row windows with halo recompute: 0 = 2 x 2 waves,
  *                  2 = 4 waves on N with 4 W k-steps in flight (C = 128; else as 0), 3 = 8 waves

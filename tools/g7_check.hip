@@ -184,10 +184,10 @@ int main(int argc, char** argv) {
   g.a[0] = g.a[1] = g.a[2] = da; g.lda[0] = g.lda[1] = g.lda[2] = K;
   g.cseg[1] = g.cseg[2] = g.cseg[3] = K; g.cin = K; g.taps = 1; g.dil = 1; g.pad = 0;
   g.M = M; g.T = M; g.N = N; g.K = K; g.Kp = K; g.ldo = N; g.act = act; g.bias = act == kActNone ? nullptr : db;
-  // mode 2: the SE-Res2Block conv3 epilogue of the model (ReLU, BN scale / shift, f64 SE column sums)
+  // mode 1: + BN scale / shift; 2: + residual; 3: + per-utterance row bias; 4: + SE column sums
   const int mode = argc > 6 ? std::atoi(argv[6]) : 0;
   float *dsc = nullptr, *dsh = nullptr;
-  double* dcs = nullptr;
+  float* dres = nullptr;
   if (mode >= 1) {
     std::vector<float> sc(N, 0.9f), sh(N, 0.01f);
     CK(hipMalloc(&dsc, N * 4)); CK(hipMalloc(&dsh, N * 4));
@@ -195,16 +195,33 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dsh, sh.data(), N * 4, hipMemcpyHostToDevice));
     g.scale = dsc; g.shift = dsh;
   }
-  if (mode >= 2) {
-    CK(hipMalloc(&dcs, (size_t)((M + 255) / 256) * 2 * N * 8));
-    g.colsum = dcs; g.T = 498;
+  if (mode == 2) {  // residual epilogue (HuBERT out_proj / fc2)
+    std::vector<float> res((size_t)M * N);
+    for (auto& x : res) x = ua(rng);
+    CK(hipMalloc(&dres, res.size() * 4));
+    CK(hipMemcpy(dres, res.data(), res.size() * 4, hipMemcpyHostToDevice));
+    g.res = dres; g.ldres = N;
+  }
+  double* dcs[3] = {nullptr, nullptr, nullptr};
+  const size_t ncs = (size_t)((M + 255) / 256) * 2 * N;
+  if (mode == 4) {  // SE column sums (the SE-Res2Block conv3 epilogue: ReLU, BN, f64 column sums)
+    for (int v = 0; v < 3; ++v) CK(hipMalloc(&dcs[v], ncs * 8));
+    g.T = 498;
+  }
+  if (mode == 3) {  // row bias per utterance of 498 rows (ECAPA conv_cat / ASTP linear1 form)
+    g.T = 498;
+    std::vector<float> rb((size_t)((M + 497) / 498) * N);
+    for (auto& x : rb) x = uw(rng);
+    CK(hipMalloc(&dres, rb.size() * 4));
+    CK(hipMemcpy(dres, rb.data(), rb.size() * 4, hipMemcpyHostToDevice));
+    g.row_bias = dres;
   }
   g = normalized(g);
   hipStream_t s; CK(hipStreamCreate(&s));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const char* names[3] = {"family6", "family7", "proto_G"};
   auto run = [&](int v) {
-    ConvGemmArgs q = g; q.out = o[v];
+    ConvGemmArgs q = g; q.out = o[v]; q.colsum = dcs[v];
     if (v == 0) x3::t_4x2_2x4_mf16(q, (const __bf16*)dh, (const __bf16*)dl, s);
     else if (v == 1) x3::t_g256(q, (const __bf16*)dh, (const __bf16*)dl, s);
     else hipLaunchKernelGGL(gemm_g<0>, dim3(((M + 255) / 256) * (N / 256)), dim3(512), 2 * GSTAGE, s, da, (const __bf16*)dh, (const __bf16*)dl, o[2], M, N, K);
@@ -226,5 +243,13 @@ int main(int argc, char** argv) {
   double d01 = 0, d02 = 0;
   for (size_t i = 0; i < r0.size(); ++i) { d01 = std::fmax(d01, std::fabs(r0[i] - r1[i])); d02 = std::fmax(d02, std::fabs(r0[i] - r2[i])); }
   std::printf("max |f6 - f7| = %.3g  max |f6 - proto| = %.3g (proto has no epilogue: equal only at act 0)\n", d01, d02);
+  if (dcs[0]) {
+    std::vector<double> c0(ncs), c1(ncs);
+    CK(hipMemcpy(c0.data(), dcs[0], ncs * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(c1.data(), dcs[1], ncs * 8, hipMemcpyDeviceToHost));
+    size_t ndiff = 0;
+    for (size_t i = 0; i < ncs; ++i) ndiff += c0[i] != c1[i];
+    std::printf("column sums: %zu of %zu differ (f6 vs f7)\n", ndiff, ncs);
+  }
   return 0;
 }

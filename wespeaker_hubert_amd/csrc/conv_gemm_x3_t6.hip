@@ -10,13 +10,17 @@
 // rows) land in the free half of a two-stage ring while the other half multiplies; a k-tile
 // ends with one vmcnt(0) + barrier and the next DMAs are issued right behind it.  The split
 // moves to the fragment reads (8 floats -> bf16x8 hi + lo per 16x16x32 A fragment), where its
-// VALU issues beside the MFMAs.  Same products, same MFMA order, same epilogue as family 6:
-// bit-identical results.  The k-loop alone (timing build without epilogue) runs 0.56-0.58 ms on
-// the C x C shape against 0.64-0.66 with plain stores and 0.69-0.72 for family 6 with the bias +
-// ReLU epilogue (tools/g7_check.hip); in the model (C2, r4) conv_cat 2.72-2.78 -> 2.69-2.70 ms,
-// C2 +0.9 %.  The epilogue (the 0.5 GB C write at one block per CU, nothing overlapping it) is
-// ~15-25 % of a block at K <= 1024; a persistent form fetching the next tile's first k-tiles
-// behind it measured no faster (profiles/r4e_gemm_family7_experiments.txt).
+// VALU issues beside the MFMAs.  Same products, same MFMA order, same per-element epilogue
+// arithmetic as family 6: bit-identical results.  The epilogue (the 256 KB C tile leaving one
+// block per CU with nothing overlapping it, ~15-25 % of a block at K <= 1024) goes through LDS
+// and leaves as whole 512-B row pieces in 16-B stores (g_epilogue_rows; the SE column sums
+// re-read the staged outputs in family 6's summation order: bit-identical f64 partials, in a
+// kernel instance of their own whose epilogue spills ~45 registers outside the k-loop).  C x C
+// conv: bias + ReLU + BN 0.69-0.70 -> 0.64-0.65 ms, + SE column sums 0.76 -> 0.69-0.72
+// (tools/g7_check); C2 +3.6 %, C4 +3.2 % against family 6 in the model.  A transposed
+// accumulator map storing 16 B per lane straight from registers (16 rows x 64 B per store) was
+// slower in the model, and a persistent form fetching the next tile's first k-tiles behind the
+// epilogue measured no faster (profiles/r4e_gemm_family7_experiments.txt).
 //
 // LDS per stage (64 KB; two stages = 128 KB, one block of 8 waves per CU):
 //   A [256 rows][32 k] fp32, 16-B chunk c of row r at slot c ^ ((r >> 1) & 5) — the two
@@ -27,7 +31,7 @@
 // chunk it fetches (cdna_hip_programming.md §5.4 rule 21).
 // Supported operands: 1-D convs with one or three concatenated A segments on 32-aligned k-tiles
 // (taps / dilation / padding / stride / ragged batches as ALoader), no added operand, no
-// grouped columns, N % 256 == 0, and an epilogue without SE column sums or residual —
+// grouped columns, N % 256 == 0, 16-B aligned epilogue operands —
 // launch_conv_gemm_x3 routes everything else to family 6.
 #include "conv_gemm_x3_impl.h"
 
@@ -45,7 +49,110 @@ __device__ __forceinline__ void g_dma(__amdgpu_buffer_rsrc_t r, unsigned char* l
 
 // DENSE: 1x1 row-local GEMMs (taps 1, no padding, stride 1: A row = output row, also in ragged
 // batches) keep one register per A row; the conv form keeps ALoader's (row, frame, length) triple.
-template <bool DENSE>
+// Epilogue through LDS: each wave parks its raw 64 x 128 accumulators, 32 rows at a time, in a
+// private [32][132] fp32 block (padded rows: the 16 column lanes x rows 4q + r of a
+// ds_write_b32 hit distinct banks), then walks them back row-major — lane l owns columns
+// 4 (l & 31) .. + 3 and rows 2u + (l >> 5) — so every epilogue operand (bias / BN / row bias /
+// residual) is one 16-B load and every output leaves in a 16-B store that, with its 31
+// neighbours, writes a whole 512-B row piece (4 full 128-B lines per row instead of 64-B pieces
+// of 4 rows per dword store).  Same per-element arithmetic and order as gemm_epilogue_store16.
+constexpr int kGEpiLd = 132;
+constexpr int kGEpiBytes = 8 * 32 * kGEpiLd * 4;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+template <int ACT, bool RB, bool RES, bool CS>
+__device__ __forceinline__ void g_epilogue_rows(const ConvGemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0, int wm,
+                                                int wn, int wave, int lane, unsigned char* smem) {
+  float* stg = reinterpret_cast<float*>(smem) + wave * 32 * kGEpiLd;
+  const int c16 = lane & 15, q = lane >> 4;
+  const int cl = 4 * (lane & 31);  // this lane's 4 columns within the wave's 128
+  const int col = n0 + wn * 128 + cl;
+  const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 sc = p.scale ? *reinterpret_cast<const f32x4*>(p.scale + col) : f32x4{1.f, 1.f, 1.f, 1.f};
+  const f32x4 sh = p.scale ? *reinterpret_cast<const f32x4*>(p.shift + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
+  const __amdgpu_buffer_rsrc_t rres = make_rsrc(RES ? p.res : p.out);
+  double cs[CS ? 8 : 1][2];
+  if constexpr (CS) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs[j][0] = cs[j][1] = 0.0;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) stg[(i2 * 16 + 4 * q + r) * kGEpiLd + j * 16 + c16] = acc[2 * h + i2][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private block: in-order LDS, no barrier
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int rl = 2 * u + (lane >> 5);
+      const int row = m0 + wm * 64 + h * 32 + rl;
+      const bool ok = row < p.M;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(stg + rl * kGEpiLd + cl);
+      f32x4 rv{0.f, 0.f, 0.f, 0.f}, rb{0.f, 0.f, 0.f, 0.f};
+      if constexpr (RES) rv = bload4(rres, ok ? (row * p.ldres + col) * 4 : kOOB);
+      if constexpr (RB) {
+        const int rowc = ok ? row : p.M - 1;
+        const int ub = p.seg ? seg_of(p.seg, p.nseg, rowc) : rowc / p.T;
+        rb = *reinterpret_cast<const f32x4*>(p.row_bias + (size_t)ub * p.N + col);
+      }
+      f32x4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = x[e] + bv[e];
+        if constexpr (RES) v += rv[e];
+        if constexpr (RB) v += rb[e];
+        if constexpr (ACT == kActRelu) v = fmaxf(v, 0.f);
+        else if constexpr (ACT == kActTanh) v = tanhf(v);
+        else if constexpr (ACT == kActGelu) v = gelu_as(v);
+        y[e] = v * sc[e] + sh[e];
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), ro, ok ? (row * p.ldo + col) * 4 : kOOB, 0,
+                                             0);
+      if constexpr (CS) {
+        *reinterpret_cast<f32x4*>(stg + rl * kGEpiLd + cl) = y;
+        if (u % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bounded read-ahead (register pressure)
+      }
+    }
+    if constexpr (CS) {
+      // SE column sums in family 6's order: lane (c16, q) adds column c16 + 16 j over rows
+      // 16 i + 4 q + r, i then r, split at the utterance boundary (gemm_epilogue_store16's
+      // per-row form; adding +0.0 for the other side leaves a sum unchanged)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // rows of this lane relative to the block: side 0 below nb (this utterance), side 1 from
+      // nb to mb (the next one); a +0.0 term for the other side, as gemm_epilogue_store16
+      const int nb = min((m0 / p.T + 1) * p.T, p.M) - m0, mb = p.M - m0;
+      const int rq = wm * 64 + 2 * h * 16 + 4 * q;
+      unsigned side0 = 0, side1 = 0;  // bit 4 i2 + r
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int rr = rq + (k >> 2) * 16 + (k & 3);
+        side0 |= (rr < nb ? 1u : 0u) << k;
+        side1 |= (rr >= nb && rr < mb ? 1u : 0u) << k;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const double yd = (double)stg[((k >> 2) * 16 + 4 * q + (k & 3)) * kGEpiLd + j * 16 + c16];
+          cs[j][0] += (side0 >> k) & 1 ? yd : 0.0;
+          cs[j][1] += (side1 >> k) & 1 ? yd : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one column's 8 reads at a time (register pressure)
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next half overwrites
+  }
+  if constexpr (CS) {
+    __syncthreads();  // the reduction buffer overlaps other waves' staging blocks
+    gemm_colsum_reduce16<8, 4, 2, 256>(p, cs, m0, n0, wm, wn, lane, smem);
+  }
+}
+
+template <bool DENSE, bool CSK>
 __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, const __bf16* __restrict__ whi,
                                                       const __bf16* __restrict__ wlo) {
   using L = Lds<true, 16>;
@@ -205,7 +312,23 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
     if (kt + 2 < nk) dma(kt + 2, buf);
   }
   // no DMA is in flight and every wave is past the last reads: the epilogue may use LDS
-  gemm_epilogue16<4, 8, 4, 2>(p, acc, m0, n0, wm, wn, lane, smem);
+#define WSP_GEPI(RB, RES, CS)                                                                                 \
+  switch (p.act) {                                                                                           \
+    case kActRelu: g_epilogue_rows<kActRelu, RB, RES, CS>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;  \
+    case kActTanh: g_epilogue_rows<kActTanh, RB, RES, CS>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;  \
+    case kActGelu: g_epilogue_rows<kActGelu, RB, RES, CS>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;  \
+    default: g_epilogue_rows<kActNone, RB, RES, CS>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;        \
+  }
+  if constexpr (CSK) {  // SE column sums: own kernel (its epilogue's register peak stays out of the others)
+    WSP_GEPI(false, false, true)
+  } else if (p.res) {
+    WSP_GEPI(false, true, false)
+  } else if (p.row_bias) {
+    WSP_GEPI(true, false, false)
+  } else {
+    WSP_GEPI(false, false, false)
+  }
+#undef WSP_GEPI
 }
 
 }  // namespace
@@ -213,17 +336,24 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
 namespace x3 {
 
 bool g256_supported(const ConvGemmArgs& p) {
-  // SE column-sum and residual epilogues measured no faster here than on family 6 (r4, in model:
-  // the epilogue, ~15-25 % of a 256 x 256 block at K <= 1024, is the same code) and stay there
-  return !p.colsum && !p.res && p.N % 256 == 0 && !p.conv2d && !p.gcols && p.amode == kACat && uniform_ktiles(p);
+  auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool aligned = a16(p.out) && p.ldo % 4 == 0 && a16(p.bias) && a16(p.scale) && a16(p.shift) &&
+                       a16(p.row_bias) && a16(p.res) && (!p.res || p.ldres % 4 == 0);
+  return aligned && p.N % 256 == 0 && !p.conv2d && !p.gcols && p.amode == kACat && uniform_ktiles(p);
 }
 
 void t_g256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s) {
   const int nwg = ((p.M + 255) / 256) * (p.N / 256);
-  if (p.taps == 1 && p.pad == 0 && p.stride == 1)
-    hipLaunchKernelGGL(conv_gemm_g<true>, dim3(nwg), dim3(512), 2 * kGStage, s, p, h, l);
+  constexpr int lds = 2 * kGStage > kGEpiBytes ? 2 * kGStage : kGEpiBytes;
+  const bool dense = p.taps == 1 && p.pad == 0 && p.stride == 1;
+  if (p.colsum && dense)
+    hipLaunchKernelGGL((conv_gemm_g<true, true>), dim3(nwg), dim3(512), lds, s, p, h, l);
+  else if (p.colsum)
+    hipLaunchKernelGGL((conv_gemm_g<false, true>), dim3(nwg), dim3(512), lds, s, p, h, l);
+  else if (dense)
+    hipLaunchKernelGGL((conv_gemm_g<true, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
   else
-    hipLaunchKernelGGL(conv_gemm_g<false>, dim3(nwg), dim3(512), 2 * kGStage, s, p, h, l);
+    hipLaunchKernelGGL((conv_gemm_g<false, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
   WSP_HIP(hipGetLastError());
 }
 
