@@ -57,13 +57,13 @@ def dominant_symbol(precision: int, variant, N: int, K: int, role: int):
     if variant == 7 and bn == 256:
         # family 7 (conv_gemm_x3_t6.hip, conv_gemm_g<DENSE, CSK>): the SE-Res2Block conv3 (role 1)
         # runs the column-sum instance
-        return G_SYMBOL + ("ILb1ELb1E" if role == 1 else "ILb1ELb0E"), bm, bn, nt
+        return G_SYMBOL + ("ILi1ELb1E" if role == 1 else "ILi1ELb0E"), bm, bn, nt
     sym = f"_ZN3wsp12_GLOBAL__N_112conv_gemm_x3{t}Li0ELb1ELi{role}E" + ("" if role else "Lb0E")
     if bn == 256:  # the 256 x 256 tile (one staging set): 32x32x16 (variant 5) or 16x16x32 (6) MFMAs
         sym += ("" if role == 0 else "Lb0E") + "Lb1ELi1E" + ("Li16E" if variant in (6, 7) else "Li32E")
     return sym, bm, bn, nt
 
-# family 7's LDS-DMA tile kernel conv_gemm_g<DENSE, CSK> (conv_gemm_x3_t6.hip)
+# family 7's LDS-DMA tile kernel conv_gemm_g<AM, CSK> (conv_gemm_x3_t6.hip; AM 1 = dense, 0 = conv)
 G_SYMBOL = "_ZN3wsp12_GLOBAL__N_111conv_gemm_g"
 HUBERT_ARCH = "HuBERT_ECAPA_GLOB_c512"  # C4: HuBERT-base front end + ECAPA_TDNN_GLOB_c512(feat_dim 768)
 HEAD_TAGS = ("layer1", "conv1x1_CxC", "res2_k3", "se", "conv_cat", "glob_ctx", "pool_linear1", "pool_linear2",
@@ -704,7 +704,7 @@ def kernel_roofline_hubert(w) -> dict:
 
     def is_c1(s, g):  # the 16x16x32 256 x 256 GELU tile at a grid of whole 7 999-row utterances
         if ("conv_gemm_x3ILi4ELi2ELi2ELi4ELi0ELb1ELi0ELb0ELb1ELi1ELi16E" not in s
-                and not s.startswith(G_SYMBOL + "ILb0ELb0E")):
+                and not s.startswith(G_SYMBOL + "ILi0ELb0E")):
             return False
         blocks = g // 512 // 2
         nb = round(blocks * 256 / t1)

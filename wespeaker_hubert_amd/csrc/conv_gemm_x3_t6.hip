@@ -29,9 +29,9 @@
 //   W hi, W lo [256 columns][32 k] bf16, family 6's {0, 2, 3, 1} row swizzle.
 // A DMA lane writes LDS base + 16 lane (lane-linear), so the swizzle is applied to the SOURCE
 // chunk it fetches (cdna_hip_programming.md §5.4 rule 21).
-// Supported operands: 1-D convs with one or three concatenated A segments on 32-aligned k-tiles
-// (taps / dilation / padding / stride / ragged batches as ALoader), no added operand, no
-// grouped columns, N % 256 == 0, 16-B aligned epilogue operands —
+// Supported operands: 1-D convs with one or three concatenated A segments on 32-aligned k-tiles,
+// or one segment on k-tiles straddling taps (taps / dilation / padding / stride / ragged batches
+// as ALoader), no added operand, no grouped columns, N % 256 == 0, 16-B aligned epilogue operands —
 // launch_conv_gemm_x3 routes everything else to family 6.
 #include "conv_gemm_x3_impl.h"
 
@@ -47,8 +47,11 @@ __device__ __forceinline__ void g_dma(__amdgpu_buffer_rsrc_t r, unsigned char* l
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, 0, 0, 0);
 }
 
-// DENSE: 1x1 row-local GEMMs (taps 1, no padding, stride 1: A row = output row, also in ragged
-// batches) keep one register per A row; the conv form keeps ALoader's (row, frame, length) triple.
+// A modes (AM): 1 = dense, 1x1 row-local GEMMs (taps 1, no padding, stride 1: A row = output row,
+// also in ragged batches) keep one register per A row; 0 = convs on uniform k-tiles (one tap and
+// one concat segment per k-tile) keep ALoader's (row, frame, length) triple; 2 = k-tiles that
+// straddle taps (cin % 32 != 0: ECAPA layer1, cin 80) decode tap and channel per lane and 16-B
+// chunk (ALoader's non-uniform path; one A segment, zeros past K).
 // Epilogue through LDS: each wave parks its raw 64 x 128 accumulators, 32 rows at a time, in a
 // private [32][132] fp32 block (padded rows: the 16 column lanes x rows 4q + r of a
 // ds_write_b32 hit distinct banks), then walks them back row-major — lane l owns columns
@@ -152,10 +155,11 @@ __device__ __forceinline__ void g_epilogue_rows(const ConvGemmArgs& p, f32x4 (&a
   }
 }
 
-template <bool DENSE, bool CSK>
+template <int AM, bool CSK>
 __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, const __bf16* __restrict__ whi,
                                                       const __bf16* __restrict__ wlo) {
   using L = Lds<true, 16>;
+  constexpr bool DENSE = AM == 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -225,6 +229,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
     for (int i = 0; i < 4; ++i) {
       if constexpr (DENSE) {
         g_dma(ra, st + (4 * wave + i) * 1024, a_r[i] >= 0 ? (a_r[i] * ld + cl + (i & 1 ? ac1 : ac0)) * 4 : kOOB);
+      } else if constexpr (AM == 2) {
+        const int k = kt * BK + (i & 1 ? ac1 : ac0);
+        const int tap = k / p.cin;
+        const int offk = tap * p.dil - p.pad;
+        const int tt = a_t[i] + offk;
+        const bool ok = k < p.K && tt >= 0 && tt < a_l[i];
+        g_dma(ra, st + (4 * wave + i) * 1024, ok ? ((a_r[i] + offk) * ld + k - tap * p.cin) * 4 : kOOB);
       } else {
         const int tt = a_t[i] + off;
         const bool ok = tt >= 0 && tt < a_l[i];
@@ -339,21 +350,25 @@ bool g256_supported(const ConvGemmArgs& p) {
   auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   const bool aligned = a16(p.out) && p.ldo % 4 == 0 && a16(p.bias) && a16(p.scale) && a16(p.shift) &&
                        a16(p.row_bias) && a16(p.res) && (!p.res || p.ldres % 4 == 0);
-  return aligned && p.N % 256 == 0 && !p.conv2d && !p.gcols && p.amode == kACat && uniform_ktiles(p);
+  // non-uniform k-tiles (AM 2): one A segment only, as ALoader's per-lane path
+  return aligned && p.N % 256 == 0 && !p.conv2d && !p.gcols && p.amode == kACat &&
+         (uniform_ktiles(p) || (p.cseg[1] >= p.cin && !p.colsum));
 }
 
 void t_g256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s) {
   const int nwg = ((p.M + 255) / 256) * (p.N / 256);
   constexpr int lds = 2 * kGStage > kGEpiBytes ? 2 * kGStage : kGEpiBytes;
-  const bool dense = p.taps == 1 && p.pad == 0 && p.stride == 1;
-  if (p.colsum && dense)
-    hipLaunchKernelGGL((conv_gemm_g<true, true>), dim3(nwg), dim3(512), lds, s, p, h, l);
-  else if (p.colsum)
-    hipLaunchKernelGGL((conv_gemm_g<false, true>), dim3(nwg), dim3(512), lds, s, p, h, l);
-  else if (dense)
-    hipLaunchKernelGGL((conv_gemm_g<true, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
+  const int am = !uniform_ktiles(p) ? 2 : p.taps == 1 && p.pad == 0 && p.stride == 1 ? 1 : 0;
+  if (p.colsum && am == 1)
+    hipLaunchKernelGGL((conv_gemm_g<1, true>), dim3(nwg), dim3(512), lds, s, p, h, l);
+  else if (p.colsum && am == 0)
+    hipLaunchKernelGGL((conv_gemm_g<0, true>), dim3(nwg), dim3(512), lds, s, p, h, l);
+  else if (am == 1)
+    hipLaunchKernelGGL((conv_gemm_g<1, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
+  else if (am == 0)
+    hipLaunchKernelGGL((conv_gemm_g<0, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
   else
-    hipLaunchKernelGGL((conv_gemm_g<false, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
+    hipLaunchKernelGGL((conv_gemm_g<2, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
   WSP_HIP(hipGetLastError());
 }
 
