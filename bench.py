@@ -822,8 +822,9 @@ def run_workload(args, arch: str, B: int, steps: int, warmup: int, world: int, r
         e_s = timed(n_s)
         sustained = {"value": round(world * B * n_s / e_s, 2), "steps": n_s, "seconds": round(e_s, 3),
                      "ms_per_step": round(e_s / n_s * 1e3, 3)}
-    if headline and args.precision == 1 and not args.no_f32:
-        # exact-f32 MFMA (precision 0) beside the bf16x3 headline
+    if headline and args.precision == 1 and not args.no_f32 and not arch.startswith(("ResNet", "SimAM")):
+        # exact-f32 MFMA (precision 0) beside the bf16x3 headline (ECAPA-TDNN / HuBERT: the ResNet
+        # families run on the bf16x3 kernels only)
         for mm in (model, fe):
             if mm is not None:
                 mm.set_option("precision", 0)

@@ -238,6 +238,7 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
   float* qkv = ws + off[5];
   float* ao = ws + off[6];
   float* ffn = ws + off[7];
+  float* cnn6 = qkv;  // [M][512] CNN output of the whole batch; qkv is first written by layer 0
   float* pc = ffn;  // the pos_conv output is consumed before fc1 writes
   int* dseg = reinterpret_cast<int*>(ws + off[8]);
   // pageable source: the copy is staged before hipMemcpyAsync returns, so pl.offs may go away
@@ -317,14 +318,17 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
     // profiling sub-classes per layer: h_cnn.c<i>
     static const char* kCnn[7] = {"", "h_cnn.c1", "h_cnn.c2", "h_cnn.c3", "h_cnn.c4", "h_cnn.c5", "h_cnn.c6"};
     for (int i = 1; i < 7; ++i) {
-      conv(kCnn[i], h_conv[i], src, kConvDim, dst, kConvDim, (int)c.rows[i], (int)c.rows[i - 1], kConvS[i], 0,
+      // the last layer writes this chunk's rows of the whole batch's CNN output (cnn6)
+      float* o = i == 6 ? cnn6 + c.row6 * kConvDim : dst;
+      conv(kCnn[i], h_conv[i], src, kConvDim, o, kConvDim, (int)c.rows[i], (int)c.rows[i - 1], kConvS[i], 0,
            kActGelu, nullptr, false, lvl(i), lvl(i - 1), nb);
       std::swap(src, dst);
     }
-    ln("h_ln", src, nullptr, src, (int)c.rows[6], kConvDim, h_ln0_g, h_ln0_b, -1);
-    conv("h_proj", h_proj, src, kConvDim, x + c.row6 * kHidden, kHidden, (int)c.rows[6], (int)c.rows[6], 1, 0,
-         kActNone, nullptr, true, nullptr, nullptr, 0);
   }
+  // LayerNorm + feature projection once over every chunk's rows (row-local: the same results as
+  // per chunk, in one launch each instead of one per chunk with a few hundred blocks)
+  ln("h_ln", cnn6, nullptr, cnn6, M, kConvDim, h_ln0_g, h_ln0_b, -1);
+  conv("h_proj", h_proj, cnn6, kConvDim, x, kHidden, M, M, 1, 0, kActNone, nullptr, true, nullptr, nullptr, 0);
   // ---- encoder: x + GELU(pos_conv(x)) -> LN  (SamePad: pad 64, last output dropped)
   conv("h_pos_conv", h_pos, x, kHidden, pc, kPosGroups * kPosGout, M, M, 1, kPosK / 2, kActGelu, nullptr, true, seg6,
        nullptr, B, kPosGout, kPosGin);
