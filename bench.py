@@ -1007,9 +1007,22 @@ def main():
 
 def summarize(res: dict) -> dict:
     def one(r, roof, kroof, cpu):
+        # ECAPA headlines carry the dominant kernel's roofline as `roofline` itself (a per-kernel
+        # figure: kernel_roofline repeats it); C3 / C4 carry a whole-model figure plus the
+        # dominant kernel's from the standalone side pass
+        per_kernel = (roof or {}).get("kernel", "").startswith("_Z")
+        if kroof is None and per_kernel:
+            kroof = roof
+        k = kroof or {}
+        mfma = k.get("bound") == "mfma"
+        # the dominant kernel on one basis for every config: issued bf16x3 MFMA work (3 bf16
+        # products per fp32 product) over the dense bf16 peak, or HBM bytes over 8 TB/s
+        kfrac = (k.get("frac_issue_peak", k.get("frac_of_issue_peak")) if mfma else k.get("frac"))
         d = {"value": r.get("value"), "ms_per_step": r.get("ms_per_step"),
              "roofline_frac": (roof or {}).get("frac"),
-             "kernel_roofline_frac": (kroof or {}).get("frac"),
+             "roofline_kind": "kernel" if per_kernel else "model",
+             "kernel_roofline_frac": kfrac,
+             "kernel_roofline_basis": ("issued bf16x3 / bf16 peak" if mfma else "HBM") if k else None,
              "cpu_baseline": (cpu or {}).get("value")}
         if (kroof or {}).get("standalone_avg_ms") is not None:
             d["kernel_ms"] = kroof["standalone_avg_ms"]
