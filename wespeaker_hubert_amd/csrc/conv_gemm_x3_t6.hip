@@ -14,10 +14,10 @@
 // arithmetic as family 6: bit-identical results.  The epilogue (the 256 KB C tile leaving one
 // block per CU with nothing overlapping it, ~15-25 % of a block at K <= 1024) goes through LDS
 // and leaves as whole 512-B row pieces in 16-B stores (g_epilogue_rows; the SE column sums
-// re-read the staged outputs in family 6's summation order: bit-identical f64 partials, in a
-// kernel instance of their own whose epilogue spills ~45 registers outside the k-loop).  C x C
-// conv: bias + ReLU + BN 0.69-0.70 -> 0.64-0.65 ms, + SE column sums 0.76 -> 0.69-0.72
-// (tools/g7_check); C2 +3.6 %, C4 +3.2 % against family 6 in the model.  A transposed
+// re-read the staged outputs in family 6's summation order — bit-identical f64 partials — in
+// two column passes of 64 (g_epilogue_cs, a kernel instance of its own) so that no sum stays
+// live across passes).  C x C conv: bias + ReLU + BN 0.69-0.70 -> 0.64-0.65 ms, + SE column
+// sums 0.78-0.80 -> 0.71-0.73 (tools/g7_check); C2 +5.2 %, C4 +3.2-3.6 % against family 6.  A transposed
 // accumulator map storing 16 B per lane straight from registers (16 rows x 64 B per store) was
 // slower in the model, and a persistent form fetching the next tile's first k-tiles behind the
 // epilogue measured no faster (profiles/r4e_gemm_family7_experiments.txt).
@@ -63,7 +63,7 @@ constexpr int kGEpiLd = 132;
 constexpr int kGEpiBytes = 8 * 32 * kGEpiLd * 4;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-template <int ACT, bool RB, bool RES, bool CS>
+template <int ACT, bool RB, bool RES>
 __device__ __forceinline__ void g_epilogue_rows(const ConvGemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0, int wm,
                                                 int wn, int wave, int lane, unsigned char* smem) {
   float* stg = reinterpret_cast<float*>(smem) + wave * 32 * kGEpiLd;
@@ -75,11 +75,6 @@ __device__ __forceinline__ void g_epilogue_rows(const ConvGemmArgs& p, f32x4 (&a
   const f32x4 sh = p.scale ? *reinterpret_cast<const f32x4*>(p.shift + col) : f32x4{0.f, 0.f, 0.f, 0.f};
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
   const __amdgpu_buffer_rsrc_t rres = make_rsrc(RES ? p.res : p.out);
-  double cs[CS ? 8 : 1][2];
-  if constexpr (CS) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) cs[j][0] = cs[j][1] = 0.0;
-  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -115,43 +110,104 @@ __device__ __forceinline__ void g_epilogue_rows(const ConvGemmArgs& p, f32x4 (&a
       }
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), ro, ok ? (row * p.ldo + col) * 4 : kOOB, 0,
                                              0);
-      if constexpr (CS) {
-        *reinterpret_cast<f32x4*>(stg + rl * kGEpiLd + cl) = y;
-        if (u % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bounded read-ahead (register pressure)
-      }
-    }
-    if constexpr (CS) {
-      // SE column sums in family 6's order: lane (c16, q) adds column c16 + 16 j over rows
-      // 16 i + 4 q + r, i then r, split at the utterance boundary (gemm_epilogue_store16's
-      // per-row form; adding +0.0 for the other side leaves a sum unchanged)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      // rows of this lane relative to the block: side 0 below nb (this utterance), side 1 from
-      // nb to mb (the next one); a +0.0 term for the other side, as gemm_epilogue_store16
-      const int nb = min((m0 / p.T + 1) * p.T, p.M) - m0, mb = p.M - m0;
-      const int rq = wm * 64 + 2 * h * 16 + 4 * q;
-      unsigned side0 = 0, side1 = 0;  // bit 4 i2 + r
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int rr = rq + (k >> 2) * 16 + (k & 3);
-        side0 |= (rr < nb ? 1u : 0u) << k;
-        side1 |= (rr >= nb && rr < mb ? 1u : 0u) << k;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const double yd = (double)stg[((k >> 2) * 16 + 4 * q + (k & 3)) * kGEpiLd + j * 16 + c16];
-          cs[j][0] += (side0 >> k) & 1 ? yd : 0.0;
-          cs[j][1] += (side1 >> k) & 1 ? yd : 0.0;
-        }
-        __builtin_amdgcn_sched_barrier(0);  // one column's 8 reads at a time (register pressure)
-      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next half overwrites
   }
-  if constexpr (CS) {
-    __syncthreads();  // the reduction buffer overlaps other waves' staging blocks
-    gemm_colsum_reduce16<8, 4, 2, 256>(p, cs, m0, n0, wm, wn, lane, smem);
+}
+
+// The SE-column-sum epilogue (CSK instances) in two column passes of 64: each wave stages its
+// 64 rows x 64 columns ([64][68] fp32), writes them out row-major (16 lanes x 16 B = 256 B per
+// row piece) and re-reads the staged outputs for the column sums of those 4 column tiles, so
+// no column sum stays live across passes (the one-pass form spilled ~130 registers).  Sums in
+// family 6's order: per lane rows 16 i + 4 q + r (i, then r), lanes l ^ 16, l ^ 32, then waves.
+constexpr int kGCsLd = 68;
+constexpr int kGCsBytes = 8 * 64 * kGCsLd * 4;
+template <int ACT>
+__device__ __forceinline__ void g_epilogue_cs(const ConvGemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0, int wm,
+                                              int wn, int wave, int lane, unsigned char* smem) {
+  float* stg = reinterpret_cast<float*>(smem) + wave * 64 * kGCsLd;
+  const int c16 = lane & 15, q = lane >> 4;
+  const int cl = 4 * c16;  // this lane's 4 columns within the pass's 64
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
+  // rows of this lane's sums relative to the block: side 0 below nb, side 1 from nb to mb
+  const int nb = min((m0 / p.T + 1) * p.T, p.M) - m0, mb = p.M - m0;
+  unsigned side0 = 0, side1 = 0;  // bit 4 i + r
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int rr = wm * 64 + (k >> 2) * 16 + 4 * q + (k & 3);
+    side0 |= (rr < nb ? 1u : 0u) << k;
+    side1 |= (rr >= nb && rr < mb ? 1u : 0u) << k;
+  }
+  double rs[8][2];
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) stg[(16 * i + 4 * q + r) * kGCsLd + 16 * jj + c16] = acc[i][4 * pp + jj][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private block: in-order LDS, no barrier
+    const int col = n0 + wn * 128 + 64 * pp + cl;
+    const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 sc = p.scale ? *reinterpret_cast<const f32x4*>(p.scale + col) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 sh = p.scale ? *reinterpret_cast<const f32x4*>(p.shift + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int rl = 4 * u + q;
+      const int row = m0 + wm * 64 + rl;
+      float* sp = stg + rl * kGCsLd + cl;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(sp);
+      f32x4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = x[e] + bv[e];
+        if constexpr (ACT == kActRelu) v = fmaxf(v, 0.f);
+        else if constexpr (ACT == kActTanh) v = tanhf(v);
+        else if constexpr (ACT == kActGelu) v = gelu_as(v);
+        y[e] = v * sc[e] + sh[e];
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), ro,
+                                             row < p.M ? (row * p.ldo + col) * 4 : kOOB, 0, 0);
+      *reinterpret_cast<f32x4*>(sp) = y;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      double c0 = 0.0, c1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const double yd = (double)stg[((k >> 2) * 16 + 4 * q + (k & 3)) * kGCsLd + 16 * jj + c16];
+        c0 += (side0 >> k) & 1 ? yd : 0.0;
+        c1 += (side1 >> k) & 1 ? yd : 0.0;
+      }
+      double v0 = c0 + __shfl_xor(c0, 16);
+      v0 += __shfl_xor(v0, 32);
+      double v1 = c1 + __shfl_xor(c1, 16);
+      v1 += __shfl_xor(v1, 32);
+      rs[4 * pp + jj][0] = v0;
+      rs[4 * pp + jj][1] = v1;
+      __builtin_amdgcn_sched_barrier(0);  // one column tile's 16 reads at a time
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass overwrites
+  }
+  __syncthreads();  // the reduction buffer overlaps other waves' staging blocks
+  constexpr int BN = 256;
+  double* red = reinterpret_cast<double*>(smem);  // [4 wm][2][BN], as gemm_colsum_reduce16
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) red[(wm * 2 + u) * BN + (wn * 8 + j) * 16 + lane] = rs[j][u];
+  }
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid < 2 * BN) {
+    const int u = tid / BN, c = tid - u * BN;
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v += red[(w * 2 + u) * BN + c];
+    p.colsum[((size_t)(m0 / 256) * 2 + u) * p.N + n0 + c] = v;
   }
 }
 
@@ -323,21 +379,26 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
     if (kt + 2 < nk) dma(kt + 2, buf);
   }
   // no DMA is in flight and every wave is past the last reads: the epilogue may use LDS
-#define WSP_GEPI(RB, RES, CS)                                                                                 \
-  switch (p.act) {                                                                                           \
-    case kActRelu: g_epilogue_rows<kActRelu, RB, RES, CS>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;  \
-    case kActTanh: g_epilogue_rows<kActTanh, RB, RES, CS>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;  \
-    case kActGelu: g_epilogue_rows<kActGelu, RB, RES, CS>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;  \
-    default: g_epilogue_rows<kActNone, RB, RES, CS>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;        \
+#define WSP_GEPI(RB, RES)                                                                                   \
+  switch (p.act) {                                                                                         \
+    case kActRelu: g_epilogue_rows<kActRelu, RB, RES>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;    \
+    case kActTanh: g_epilogue_rows<kActTanh, RB, RES>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;    \
+    case kActGelu: g_epilogue_rows<kActGelu, RB, RES>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;    \
+    default: g_epilogue_rows<kActNone, RB, RES>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;          \
   }
-  if constexpr (CSK) {  // SE column sums: own kernel (its epilogue's register peak stays out of the others)
-    WSP_GEPI(false, false, true)
+  if constexpr (CSK) {  // SE column sums: own kernel instance (its epilogue's registers stay out of the others)
+    switch (p.act) {
+      case kActRelu: g_epilogue_cs<kActRelu>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;
+      case kActTanh: g_epilogue_cs<kActTanh>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;
+      case kActGelu: g_epilogue_cs<kActGelu>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;
+      default: g_epilogue_cs<kActNone>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;
+    }
   } else if (p.res) {
-    WSP_GEPI(false, true, false)
+    WSP_GEPI(false, true)
   } else if (p.row_bias) {
-    WSP_GEPI(true, false, false)
+    WSP_GEPI(true, false)
   } else {
-    WSP_GEPI(false, false, false)
+    WSP_GEPI(false, false)
   }
 #undef WSP_GEPI
 }
@@ -357,7 +418,8 @@ bool g256_supported(const ConvGemmArgs& p) {
 
 void t_g256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s) {
   const int nwg = ((p.M + 255) / 256) * (p.N / 256);
-  constexpr int lds = 2 * kGStage > kGEpiBytes ? 2 * kGStage : kGEpiBytes;
+  constexpr int lds0 = 2 * kGStage > kGEpiBytes ? 2 * kGStage : kGEpiBytes;
+  constexpr int lds = lds0 > kGCsBytes ? lds0 : kGCsBytes;
   const int am = !uniform_ktiles(p) ? 2 : p.taps == 1 && p.pad == 0 && p.stride == 1 ? 1 : 0;
   if (p.colsum && am == 1)
     hipLaunchKernelGGL((conv_gemm_g<1, true>), dim3(nwg), dim3(512), lds, s, p, h, l);
