@@ -242,9 +242,10 @@ def parse():
                     help="skip the C4 side measurement at the survey's per-rank batch 64")
     ap.add_argument("--sustain-seconds", type=float, default=2.0,
                     help="extra untimed-for-value window reported as value_sustained (>= this many seconds)")
-    ap.add_argument("--configs", default="C3,C4",
+    ap.add_argument("--configs", default="C3,C4,C5",
                     help="sub-configurations timed after the C2 headline (C3 = ResNet293 B=128, C4 = HuBERT-base + "
-                         "ECAPA_TDNN_GLOB_c512 B=256), comma-separated, or 'none'")
+                         "ECAPA_TDNN_GLOB_c512 B=256, C5 = the vox1-O-shaped extract + score + AS-Norm pipeline "
+                         "through the product's file path), comma-separated, or 'none'")
     ap.add_argument("--sub-steps", type=int, default=10)
     ap.add_argument("--sub-warmup", type=int, default=2)
     ap.add_argument("--sub-cpu-seconds", type=float, default=10.0)
@@ -978,6 +979,12 @@ def main():
     if subs:
         res["configs"] = {}
         for name in subs:
+            if name == "C5":
+                # BASELINE.json configs[4]: end-to-end seconds by stage (scripts/bench_c5.py)
+                sys.path.insert(0, os.path.join(REPO, "scripts"))
+                import bench_c5
+                res["configs"][name] = bench_c5.run_c5("ECAPA_TDNN_c1024", dev, world, rank, dist)
+                continue
             if name not in SUB_CONFIGS:
                 raise SystemExit(f"bench.py: unknown --configs entry {name} (known: {sorted(SUB_CONFIGS)})")
             sarch, sb = SUB_CONFIGS[name]
@@ -1031,6 +1038,11 @@ def summarize(res: dict) -> dict:
     if res.get("value_batch64"):
         out[res["config"]["arch"]]["value_batch64"] = res["value_batch64"]["value"]
     for name, r in (res.get("configs") or {}).items():
+        if name == "C5":
+            if r:
+                out[name] = {"seconds": r.get("value"), "stages_s": r.get("stages_s"),
+                             "eval_emb_per_s": r.get("eval_emb_per_s")}
+            continue
         out[name] = one(r, r.get("roofline"), r.get("kernel_roofline"), r.get("cpu_baseline"))
         if r.get("value_batch64"):
             out[name]["value_batch64"] = r["value_batch64"]["value"]

@@ -211,14 +211,11 @@ def extract(config="conf/config.yaml", **kwargs):
             return embed_scp
         keys, wavs = [], []
         for key, x in checked(stream):
-            if batch_size == 1:
-                run([key], [x], writer)
-            else:
-                keys.append(key)
-                wavs.append(get_random_chunk(x, chunk_len, rng))
-                if len(keys) == batch_size:
-                    run(keys, wavs, writer)
-                    keys, wavs = [], []
+            keys.append(key)
+            wavs.append(get_random_chunk(x, chunk_len, rng))
+            if len(keys) == batch_size:
+                run(keys, wavs, writer)
+                keys, wavs = [], []
             n += 1
         if keys:
             run(keys, wavs, writer)
