@@ -126,3 +126,11 @@ def test_c2_ecapa_c1024_bench_batch_rows():
 
 def test_c3_resnet293_two_chunk_rows():
     _rows_vs_one_and_oracle("ResNet293", 128, (0, 63, 64, 127), 1234, True, feat_dim=80, embed_dim=256)
+
+
+def test_ecapa_c1024_batch_beyond_2gib_runs_in_chunks():
+    """B = 640 x 5 s: the [M][1536] ASTP operands exceed 2 GiB (32-bit buffer offsets), so the
+    forward runs two 320-utterance chunks over one chunk-sized workspace; rows on both sides of
+    the chunk seam equal their batch-of-one embeddings and the oracle (bin/extract.py:90-120
+    feeds batches of any size)."""
+    _rows_vs_one_and_oracle("ECAPA_TDNN_c1024", 640, (0, 319, 320, 639), 4321, False, feat_dim=80, embed_dim=192)

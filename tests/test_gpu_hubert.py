@@ -224,15 +224,17 @@ def test_c4_bench_shape_rows_match_oracle(sd_np, sd_t):
 
 def test_lds_dma_tile_bit_identical_to_register_staged(sd_np):
     """The front end on x3_variant 7 (default: the GEMMs family 7 takes staged by LDS-DMA, the rest
-    on 6) equals x3_variant 6 bit for bit (same products, same MFMA order), ragged batch included."""
+    on 6) and 8 (7 with the SIMD partners one barrier apart) equals x3_variant 6 bit for bit (same
+    products, same MFMA order), ragged batch included."""
     lens = [16000, 12345, 48000, 700]
     wavs = [_wav(70 + i, 1, n)[0] for i, n in enumerate(lens)]
     got = []
-    for v in (6, 7):
+    for v in (6, 7, 8):
         fe = _frontend(sd_np)
         fe.set_option("x3_variant", v)
         feats, offs = fe.extract_segments([torch.from_numpy(w) for w in wavs], cmn=True)
         uni = fe.extract(torch.from_numpy(_wav(75, 3, 32000)).to(DEV), cmn=True)
         got.append((feats.cpu().numpy(), uni.cpu().numpy()))
-    np.testing.assert_array_equal(got[0][0], got[1][0])
-    np.testing.assert_array_equal(got[0][1], got[1][1])
+    for g in got[1:]:
+        np.testing.assert_array_equal(got[0][0], g[0])
+        np.testing.assert_array_equal(got[0][1], g[1])

@@ -179,6 +179,7 @@ int main(int argc, char** argv) {
   if (want("fc1")) cases.push_back(make("fc1", 256, 249, 249, 1, 768, 1, 1, 0, 3072, kActGelu, false, false, false, false, 1, nullptr));
   if (want("fc2")) cases.push_back(make("fc2", 256, 249, 249, 1, 3072, 1, 1, 0, 768, kActNone, false, false, true, false, 1, nullptr));
   if (want("qkv")) cases.push_back(make("qkv", 256, 249, 249, 1, 768, 1, 1, 0, 2304, kActNone, false, false, false, false, 1, nullptr));
+  if (want("out_proj")) cases.push_back(make("out_proj", 256, 249, 249, 1, 768, 1, 1, 0, 768, kActNone, false, false, true, false, 1, nullptr));
   if (want("cnn_c1")) cases.push_back(make("cnn_c1", 51, 7999, 15999, 2, 512, 3, 1, 0, 512, kActGelu, false, false, false, false, 1, nullptr));
   // operand forms no shipped model sends to families 7 / 8
   if (want("rb_ragged")) cases.push_back(make("rb_ragged", 0, 0, 0, 1, 512, 1, 1, 0, 512, kActRelu, true, false, false, true, 1, &ragged));

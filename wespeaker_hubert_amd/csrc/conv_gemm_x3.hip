@@ -80,7 +80,7 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
   } else if (p.gcols) {
     // grouped (HuBERT pos_conv: 16 groups x 64 padded columns, K = 48 x 128): 256-row
     // blocks halve the per-row re-reads of the group's 1.5 MB weight slice
-    f = variant == 5 ? x3::t_8x1_1x2_sw : x3::t_4x1_1x2;  // blocks stay inside one group
+    f = variant >= 5 ? x3::t_8x1_1x2_sw : x3::t_4x1_1x2;  // blocks stay inside one group
   } else if (p.N % 128 != 0) {
     f = x3::t_4x1_1x2;  // 128 x 64, 4 waves
   } else if (variant == 3) {

@@ -266,8 +266,11 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
     g.seg = oseg;  // taps==1 projections pass null: row-local, no utterance structure needed
     g.iseg = iseg;
     g.nseg = nseg;
-    // the long-K / GELU GEMMs (CNN, fc1, fc2) on the 16x16x32 form of the 256 x 256 tile (r3 A/B:
-    // CNN -2 %, fc1 -3 %, fc2 -6 % per launch); QKV / out_proj measured slower on it and stay on 32x32
+    // x3_variant 5 only: the long-K / GELU GEMMs (CNN, fc1, fc2) on the 16x16x32 form of the 256 x 256
+    // tile (r3 A/B: CNN -2 %, fc1 -3 %, fc2 -6 % per launch), QKV / out_proj on 32x32.  Under the
+    // default 7 (and 8) every one of these GEMMs (N % 256 == 0) takes the LDS-DMA 16x16x32 tile, which
+    // is faster than the register-staged 16x16x32 tile for QKV and out_proj too (tools/gemm_check,
+    // profiles/r5a_gemm_check.txt: qkv / out_proj / fc1 / fc2 / cnn.c1 per launch, families 6 vs 7)
     const bool mf16 = x3_variant == 5 && (std::strncmp(tag, "h_cnn", 5) == 0 || std::strcmp(tag, "h_fc1") == 0 ||
                                           std::strcmp(tag, "h_fc2") == 0);
     run(tag, 2.0 * rows * (gcols ? (double)cw.N * kPosGin / kPosGout : cw.N) * cw.K, s, [&] {

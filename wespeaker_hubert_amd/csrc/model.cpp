@@ -142,7 +142,8 @@ int Model::feat_dim() const { return impl->feat_dim; }
 
 // workspace of one sub-batch of B utterances, 256-byte granules
 size_t Model::Impl::ws_bytes_one(int B, int T) const {
-  const size_t f = ecapa   ? ecapa_ws_floats(B, (size_t)B * T, nullptr)
+  const int bc = ecapa ? ecapa_chunk(B, T) : B;
+  const size_t f = ecapa   ? ecapa_ws_floats(bc, (size_t)bc * T, nullptr)
                    : simam ? simam_ws_floats(B, T, nullptr)
                            : resnet_ws_floats(B, T, nullptr);
   return (f * sizeof(float) + 255) & ~size_t(255);
@@ -175,9 +176,13 @@ void Model::forward(const float* feats, int B, int T, float* embed, void* ws, si
     float* e = embed + (size_t)b0 * m.embed_dim;
     float* wsf = reinterpret_cast<float*>(wsb);
     const hipStream_t si = m.sub(s, i);
-    if (m.ecapa)
-      m.forward_ecapa(f, nb, T, e, wsf, si);
-    else if (m.simam)
+    if (m.ecapa) {
+      // consecutive utterance chunks whose operands stay < 2 GiB, over one chunk-sized workspace
+      const int bc = m.ecapa_chunk(nb, T);
+      for (int c0 = 0; c0 < nb; c0 += bc)
+        m.forward_ecapa(f + (size_t)c0 * T * m.feat_dim, std::min(bc, nb - c0), T, e + (size_t)c0 * m.embed_dim, wsf,
+                        si);
+    } else if (m.simam)
       m.forward_simam(f, nb, T, e, wsf, si);
     else
       m.forward_resnet(f, nb, T, e, wsf, si);

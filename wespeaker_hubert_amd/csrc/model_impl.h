@@ -1096,6 +1096,16 @@ struct Model::Impl {
   }
 
   // M = frame rows of the batch (B * T, or the segment total)
+  // utterances per ECAPA forward chunk (uniform batches): every activation operand, the widest
+  // being the [M][1536] ASTP input / logits, must stay < 2 GiB (32-bit buffer offsets); larger
+  // batches run as consecutive chunks over one chunk-sized workspace (as resnet_chunk)
+  int ecapa_chunk(int B, int T) const {
+    const size_t per = (size_t)T * std::max(C, 1536) * sizeof(float);
+    int bc = (int)std::max<size_t>(1, ((size_t)1 << 31) / 8 * 7 / per);
+    bc = std::min(bc, B);
+    const int chunks = (B + bc - 1) / bc;
+    return (B + chunks - 1) / chunks;
+  }
   size_t ecapa_ws_floats(int B, size_t M, size_t* offs) const {
     const size_t sizes[] = {M * C, M * C, M * C, M * C,           // x1..x4
                             M * C, M * C, M * C,                   // h1..h3
