@@ -41,9 +41,9 @@ HBM_PEAK_GBPS = 8000.0
 def x3_tile(variant, N: int, K: int, gelu: bool = False):
     """(template prefix, BM, BN, threads) of the bf16x3 block launch_conv_gemm_x3 picks."""
     v = 5 if variant is None else variant
-    if v in (5, 6, 7, 8) and N % 256 == 0:
+    if v in (5, 6, 7) and N % 256 == 0:
         return "ILi4ELi2ELi2ELi4E", 256, 256, 512
-    if v in (1, 4, 5, 6, 7, 8):
+    if v in (1, 4, 5, 6, 7):
         return "ILi4ELi2ELi2ELi2E", 256, 128, 512
     return "ILi2ELi2ELi2ELi2E", 128, 128, 256
 
@@ -54,18 +54,17 @@ def dominant_symbol(precision: int, variant, N: int, K: int, role: int, se_fused
     if precision == 0:
         return "_ZN3wsp12_GLOBAL__N_113conv_gemm_f32ILi2ELi2ELi2ELi2ELi0ELb1E", 128, 128, 256
     t, bm, bn, nt = x3_tile(variant, N, K, gelu=(role == 0))  # role 0 here = HuBERT fc1 (GELU)
-    if variant in (7, 8) and bn == 256:
-        # families 7 / 8 (conv_gemm_x3_t6.hip, conv_gemm_g<AM, CSK, PP>, AM 1 = dense 1x1): the
-        # SE-Res2Block conv3 (role 1) runs the column-sum instance when the SE squeeze is fused
-        # (uniform batches with T >= 256 rows), the plain one otherwise
-        csk = role == 1 and se_fused
-        return G_SYMBOL + ("ILi1ELb1E" if csk else "ILi1ELb0E") + ("Lb1E" if variant == 8 else "Lb0E"), bm, bn, nt
+    if variant == 7 and bn == 256:
+        # family 7 (conv_gemm_x3_t6.hip, conv_gemm_g<AM, CSK>, AM 1 = dense 1x1): the SE-Res2Block
+        # conv3 (role 1) runs the column-sum instance when the SE squeeze is fused (uniform batches
+        # with T >= 256 rows), the plain one otherwise
+        return G_SYMBOL + ("ILi1ELb1E" if role == 1 and se_fused else "ILi1ELb0E"), bm, bn, nt
     sym = f"_ZN3wsp12_GLOBAL__N_112conv_gemm_x3{t}Li0ELb1ELi{role}E" + ("" if role else "Lb0E")
     if bn == 256:  # the 256 x 256 tile (one staging set): 32x32x16 (variant 5) or 16x16x32 (6) MFMAs
         sym += ("" if role == 0 else "Lb0E") + "Lb1ELi1E" + ("Li16E" if variant in (6, 7) else "Li32E")
     return sym, bm, bn, nt
 
-# families 7 / 8's LDS-DMA tile kernel conv_gemm_g<AM, CSK, PP> (conv_gemm_x3_t6.hip; AM 1 = dense, 0 = conv)
+# family 7's LDS-DMA tile kernel conv_gemm_g<AM, CSK> (conv_gemm_x3_t6.hip; AM 1 = dense, 0 = conv)
 G_SYMBOL = "_ZN3wsp12_GLOBAL__N_111conv_gemm_g"
 HUBERT_ARCH = "HuBERT_ECAPA_GLOB_c512"  # C4: HuBERT-base front end + ECAPA_TDNN_GLOB_c512(feat_dim 768)
 HEAD_TAGS = ("layer1", "conv1x1_CxC", "res2_k3", "se", "conv_cat", "glob_ctx", "pool_linear1", "pool_linear2",
@@ -708,7 +707,7 @@ def kernel_roofline_hubert(w) -> dict:
 
     def is_c1(s, g):  # the 16x16x32 256 x 256 GELU tile at a grid of whole 7 999-row utterances
         if ("conv_gemm_x3ILi4ELi2ELi2ELi4ELi0ELb1ELi0ELb0ELb1ELi1ELi16E" not in s
-                and not s.startswith(G_SYMBOL + "ILi0ELb0E")):  # conv_gemm_g<0, false, PP>
+                and not s.startswith(G_SYMBOL + "ILi0ELb0E")):  # conv_gemm_g<0, false>
             return False
         blocks = g // 512 // 2
         nb = round(blocks * 256 / t1)
@@ -718,10 +717,9 @@ def kernel_roofline_hubert(w) -> dict:
     if pmc:
         nb = round(grid // 1024 * 256 / t1)
         pmc_algo = 4.0 * 512 * (t0 + t1) * nb
-    fam = fe.get_option("x3_variant")
-    name = (f"conv_gemm_g<0, false, {'true' if fam == 8 else 'false'}> (family {fam}: 256 x 256 tile, operands by "
-            "LDS-DMA, bf16x3 on 16x16x32 MFMAs), h_cnn.c1" if fam in (7, 8) else
-            "conv_gemm_x3<4,2,2,4,...,MF=16> (256 x 256 tile, bf16x3 on 16x16x32 MFMAs), h_cnn.c1")
+    fam7 = fe.get_option("x3_variant") == 7
+    name = ("conv_gemm_g<0, false> (family 7: 256 x 256 tile, operands by LDS-DMA, bf16x3 on 16x16x32 MFMAs), "
+            "h_cnn.c1" if fam7 else "conv_gemm_x3<4,2,2,4,...,MF=16> (256 x 256 tile, bf16x3 on 16x16x32 MFMAs), h_cnn.c1")
     rec = kernel_roofline_record(name,
                                  "h_cnn.c1", k["launches_per_step"], k["avg_ms"], algo, flops, pmc, src, pmc_algo, "mfma")
     rec["note"] = (f"{utts:.0f} utterances per launch (feature-extractor chunk); standalone = option streams 1 "

@@ -1,9 +1,10 @@
 // Development check + microbenchmark (not part of the product): the product's bf16x3 GEMM tile
-// families 6 (conv_gemm_x3_t5.hip, register-staged), 7 (conv_gemm_x3_t6.hip, LDS-DMA) and 8
-// (family 7 with the SIMD partners one barrier apart) on the operand shapes the models launch,
-// plus the operand forms only tests reach (ragged row bias, 1x1 with Ti != T).  Families 7 / 8
-// must equal family 6 bit for bit (outputs and SE column sums); then interleaved timing rounds.
-//   gemm_check [case|all] [reps] [variants, e.g. 678]
+// families 6 (conv_gemm_x3_t5.hip, register-staged) and 7 (conv_gemm_x3_t6.hip, LDS-DMA) on the
+// operand shapes the models launch, plus the operand forms only tests reach (ragged row bias,
+// 1x1 with Ti != T).  Family 7 must equal family 6 bit for bit (outputs and SE column sums); then
+// interleaved timing rounds.  (r5's family 8, a ping-pong k-loop, was measured with this tool and
+// pruned: profiles/r5a_gemm_check.txt.)
+//   gemm_check [case|all] [reps] [variants, e.g. 67]
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -155,8 +156,7 @@ void run(const Case& c, int v, float* out, double* cs, hipStream_t s) {
   if (v == 6) x3::t_4x2_2x4_mf16(q, c.whi, c.wlo, s);
   else {
     if (!x3::g256_supported(q)) { std::fprintf(stderr, "%s: family %d does not take these operands\n", c.name.c_str(), v); std::exit(2); }
-    if (v == 7) x3::t_g256(q, c.whi, c.wlo, s);
-    else x3::t_g256pp(q, c.whi, c.wlo, s);
+    x3::t_g256(q, c.whi, c.wlo, s);
   }
 }
 }  // namespace
@@ -164,7 +164,7 @@ void run(const Case& c, int v, float* out, double* cs, hipStream_t s) {
 int main(int argc, char** argv) {
   const std::string which = argc > 1 ? argv[1] : "all";
   const int reps = argc > 2 ? std::atoi(argv[2]) : 10;
-  const std::string vs = argc > 3 ? argv[3] : "678";
+  const std::string vs = argc > 3 ? argv[3] : "67";
   std::vector<int> vars;
   for (char ch : vs) vars.push_back(ch - '0');
   const std::vector<int> ragged = {300, 257, 511, 123, 800, 6};
@@ -227,35 +227,6 @@ int main(int argc, char** argv) {
       if (cs[v]) CK(hipFree(cs[v]));
     }
   }
-#ifdef WSP_G_STAMPS
-  {  // family 8 once more, then the barrier-to-barrier cycles of waves 0 / 4 by phase slot
-    const Case& c = cases[0];
-    float* o;
-    CK(hipMalloc(&o, c.out_words * 4));
-    double* csb = nullptr;
-    if (c.cs_words) CK(hipMalloc(&csb, c.cs_words * 4));
-    run(c, 8, o, csb, s);
-    CK(hipStreamSynchronize(s));
-    static unsigned long long st[1024][2][320];
-    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
-    const int nk = c.g.Kp / 32, nb = 2 + 8 * nk;
-    for (int w = 0; w < 2; ++w) {
-      double sum[8] = {0}, tot = 0;
-      int n[8] = {0};
-      for (int b = 0; b < 256; ++b) {
-        for (int j = 1 + w; j + 1 < nb - 1; ++j) {  // loop barriers only
-          const double d = (double)(st[b][w][j + 1] - st[b][w][j]);
-          const int ph = (j - w) & 7;
-          sum[ph] += d; n[ph]++;
-        }
-        tot += (double)(st[b][w][nb - 1] - st[b][w][0]);
-      }
-      std::printf("wave %d: loop cycles per block %.0f; per k-tile by segment (R0 M0 R1 M1 R2 M2 R3 M3):", 4 * w, tot / 256);
-      for (int k = 0; k < 8; ++k) std::printf(" %.0f", sum[k] / (n[k] ? n[k] : 1));
-      std::printf("\n");
-    }
-  }
-#endif
   std::printf(bad ? "MISMATCH in %d comparisons\n" : "all families bit-identical\n", bad);
   return bad ? 1 : 0;
 }

@@ -62,19 +62,18 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
               "conv_gemm_x3: column sums need a uniform batch with T >= block rows and no row bias");
   }
   WSP_CHECK(p.Kp % 64 == 0, "conv_gemm_x3: packed K must be a multiple of 64");
-  WSP_CHECK(variant >= 3 && variant <= 8, "conv_gemm_x3: tile family must be 3, 4, 5, 6, 7 or 8");
+  WSP_CHECK(variant >= 3 && variant <= 7, "conv_gemm_x3: tile family must be 3, 4, 5, 6 or 7");
   const __bf16* h = static_cast<const __bf16*>(whi);
   const __bf16* l = static_cast<const __bf16*>(wlo);
   x3::TileFn f;
-  if (variant >= 7 && x3::g256_supported(p)) {
+  if (variant == 7 && x3::g256_supported(p)) {
     // variant 7 (r4): the 256 x 256 16x16x32 tile with every operand staged by LDS-DMA and the
     // fp32 A split at fragment time (conv_gemm_x3_t6.hip); bit-identical to 6, which serves
-    // the operands it does not take (2-D, added operand, grouped, N % 256 != 0).  Variant 8
-    // (r5): the same tile with the SIMD partners' k-loops one barrier apart (ping-pong).
-    (variant == 8 ? x3::t_g256pp : x3::t_g256)(p, h, l, s);
+    // the operands it does not take (2-D, added operand, grouped, N % 256 != 0)
+    x3::t_g256(p, h, l, s);
     return;
   }
-  if (variant >= 7) variant = 6;
+  if (variant == 7) variant = 6;
   if (p.N % 64 != 0 || (p.gcols && p.gcols % 64 != 0)) {
     f = x3::t_4x1_1x1;  // 128 x 32, 4 waves
   } else if (p.gcols) {

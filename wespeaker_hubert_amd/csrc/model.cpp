@@ -264,11 +264,11 @@ void Model::set_option(const std::string& key, int value) {
               "or 4 (halo-free strips, c1024 widths; else as 3)");
     impl->res2_variant = value;
   } else if (key == "x3_variant") {
-    WSP_CHECK((value >= 0 && value <= 8) || value == 9,
-              "x3_variant must be 3, 4, 5, 6 (5 on 16x16x32 MFMAs), 7 (6 staged by LDS-DMA) or 8 (7 with "
-              "the SIMD partners one barrier apart)");
-    // 0 / 1 (unswizzled tiles), 2 / 9 (the r2 LDS-DMA tiles): pruned in r3, deprecated aliases of 5
-    impl->x3_variant = value >= 3 && value <= 8 ? value : 5;
+    WSP_CHECK((value >= 0 && value <= 9),
+              "x3_variant must be 3, 4, 5, 6 (5 on 16x16x32 MFMAs) or 7 (6 staged by LDS-DMA)");
+    // 0 / 1 (unswizzled tiles), 2 / 9 (the r2 LDS-DMA tiles): pruned in r3; 8 (the r5 ping-pong form
+    // of 7, bit-identical and slower): pruned in r5 — deprecated aliases of 5 / 7
+    impl->x3_variant = value >= 3 && value <= 7 ? value : value == 8 ? 7 : 5;
   } else if (key == "attn_lds" || key == "conv1x1_rows") {
     // pruned in r3 (hubert.hip's streaming mha_kernel, conv1x1_rows.hip): accepted, no effect
   } else {
