@@ -168,11 +168,15 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *   "attn_pipe"    HuBERT front end: 1 = the persistent pipelined attention kernel (keys in
  *                  LDS halves of 128 frames, the next half in flight; default), 0 = one block
  *                  per (utterance, head, 128-query block); both bf16x3 MFMA
+ *   "pos_conv"     HuBERT front end, precision 1: 1 = the positional conv as a direct grouped
+ *                  conv (pos_conv.hip: one block per 256 frames x group, input patch split into
+ *                  bf16 hi / lo once in LDS; default), 0 = the grouped implicit GEMM (48 of 64
+ *                  padded columns per group); equal up to fp32 rounding
  *   "layer"        HuBERT front end only, before finalize: -1 = weighted sum of all
  *                  hidden states (default), k = hidden state k alone (s3prl.py:84-87)
  * Deprecated (accepted, mapped to the shipped kernels since r3 pruned the others):
  *   "attn_lds" and "conv1x1_rows" (any value: no effect), "astp_fused" 2 / 3 (= 1),
- *   "x3_variant" 0 / 1 / 2 / 9 (= 5). */
+ *   "x3_variant" 0 / 1 / 2 / 9 (= 5), 8 (= 7). */
 int wsp_model_set_option(wsp_model* m, const char* key, int value);
 /* The current value of a runtime option above (the per-architecture default until set). */
 int wsp_model_get_option(const wsp_model* m, const char* key, int* value);

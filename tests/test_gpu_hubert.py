@@ -237,3 +237,30 @@ def test_lds_dma_tile_bit_identical_to_register_staged(sd_np):
     for g in got[1:]:
         np.testing.assert_array_equal(got[0][0], g[0])
         np.testing.assert_array_equal(got[0][1], g[1])
+
+
+@pytest.mark.parametrize("layer", [0, -1])
+def test_direct_pos_conv_matches_grouped_gemm_and_oracle(sd_np, sd_t, layer):
+    """pos_conv.hip (option pos_conv 1, default: one block per 256 frames x group, the input patch
+    split once into LDS) against the grouped implicit GEMM (pos_conv 0) and the oracle, on a ragged
+    batch with utterances of 1 .. 3 frame windows (100000 samples = 312 frames; 700 -> 2 frames)
+    and a uniform one.  Hidden state 0 is LayerNorm(x + GELU(pos_conv(x))): the kernel's output one
+    LayerNorm away."""
+    lens = [100000, 700, 16000, 250000, 12345]
+    wavs = [_wav(80 + i, 1, n)[0] for i, n in enumerate(lens)]
+    outs = []
+    for pc in (1, 0):
+        fe = _frontend(sd_np, layer=layer, multilayer=layer < 0)
+        fe.set_option("pos_conv", pc)
+        assert fe.get_option("pos_conv") == pc
+        feats, offs = fe.extract_segments([torch.from_numpy(w) for w in wavs])
+        outs.append((feats.cpu(), offs))
+    (a, offs), (b, _) = outs
+    assert (a - b).abs().max().item() <= 2e-5
+    for i in (0, 1, 3):
+        with torch.no_grad():
+            if layer < 0:
+                ref = hubert_ref.s3prl_frontend(torch.from_numpy(wavs[i][None]), sd_t)[0]
+            else:
+                ref = hubert_ref.s3prl_upstream(torch.from_numpy(wavs[i][None]), sd_t)[layer][0]
+        assert (a[offs[i]:offs[i + 1]] - ref).abs().max().item() <= FEAT_ATOL, i

@@ -333,8 +333,17 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
   ln("h_ln", cnn6, nullptr, cnn6, M, kConvDim, h_ln0_g, h_ln0_b, -1);
   conv("h_proj", h_proj, cnn6, kConvDim, x, kHidden, M, M, 1, 0, kActNone, nullptr, true, nullptr, nullptr, 0);
   // ---- encoder: x + GELU(pos_conv(x)) -> LN  (SamePad: pad 64, last output dropped)
-  conv("h_pos_conv", h_pos, x, kHidden, pc, kPosGroups * kPosGout, M, M, 1, kPosK / 2, kActGelu, nullptr, true, seg6,
-       nullptr, B, kPosGout, kPosGin);
+  if (precision == 1 && pos_conv) {
+    // direct grouped conv over the same packed weights (pos_conv.hip): 48 of 64 columns per group
+    // computed, input patch split once per block
+    run("h_pos_conv", 2.0 * M * kHidden * (double)h_pos.K, s, [&] {
+      launch_hubert_pos_conv(x, kHidden, seg6, B, pl.maxT6, M, h_pos.whi, h_pos.wlo, h_pos.Kp, kPosGout, h_pos.bias,
+                             pc, kPosGroups * kPosGout, s);
+    });
+  } else {
+    conv("h_pos_conv", h_pos, x, kHidden, pc, kPosGroups * kPosGout, M, M, 1, kPosK / 2, kActGelu, nullptr, true,
+         seg6, nullptr, B, kPosGout, kPosGin);
+  }
   ln("h_ln", x, pc, x, M, kHidden, h_enc_g, h_enc_b, 0);
   for (int l = 0; l < kLayers; ++l) {
     const HLayer& L = h_layers[l];

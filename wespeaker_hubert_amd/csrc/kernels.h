@@ -165,6 +165,13 @@ void launch_hubert_conv0(const float* wav, int B, int N, int ldw, int T0, const 
                          const int* oseg = nullptr);
 // doubles of launch_hubert_conv0's `stats` scratch for B utterances of at most T0 conv0 frames
 size_t hubert_conv0_stats_doubles(int B, int T0);
+// Positional conv (pos_conv.hip): out[row][g*gout + n] = GELU(bias[g*gout + n] + sum_{tap, c}
+// x[row + tap - 64][48 g + c] * W[g*gout + n][tap*48 + c]) for the 16 groups x 48 outputs, per
+// utterance of seg (int32 [B+1] device offsets, at most maxT frames, M rows in all); W = the
+// bf16 hi / lo grouped pack (ldw elements per row), bf16x3 products.
+void launch_hubert_pos_conv(const float* x, int ldx, const int* seg, int B, int maxT, int M, const void* whi,
+                            const void* wlo, int ldw, int gout, const float* bias, float* out, int ldo,
+                            hipStream_t s);
 // out[row] = LayerNorm(x[row] (+ add[row][remap(c)])) with remap(c) = (c/gin)*gout + c%gin;
 // if feat: feat[b][t'] (=|+=) feat_w * out[row] for t' = t, and t' in [T, Tout) when t = T-1.
 struct LayerNormArgs {

@@ -207,6 +207,7 @@ struct Model::Impl {
   std::vector<float> h_fw;  // featurizer weight per hidden state
   int h_layer_sel = -1;     // s3prl `layer` (-1: softmax-weighted sum of all 13)
   int attn_pipe = 1;        // attn.hip: 1 = persistent pipelined kernel, 0 = one block per (utterance, head)
+  int pos_conv = 1;         // HuBERT pos_conv: 1 = direct grouped conv (pos_conv.hip), 0 = grouped implicit GEMM
   void build_hubert_params();
   void finalize_hubert();
   int hubert_cnn_frames(int N, int upto) const;
