@@ -224,13 +224,15 @@ def test_c4_bench_shape_rows_match_oracle(sd_np, sd_t):
 
 def test_lds_dma_tile_bit_identical_to_register_staged(sd_np):
     """The front end on x3_variant 7 (default: the GEMMs family 7 takes staged by LDS-DMA, the rest
-    on 6) equals x3_variant 6 bit for bit (same products, same MFMA order), ragged batch included."""
+    on 6) equals x3_variant 6 bit for bit (same products, same MFMA order), ragged batch included
+    (LayerNorm fold off: it exists on family 7 only)."""
     lens = [16000, 12345, 48000, 700]
     wavs = [_wav(70 + i, 1, n)[0] for i, n in enumerate(lens)]
     got = []
     for v in (6, 7):
         fe = _frontend(sd_np)
         fe.set_option("x3_variant", v)
+        fe.set_option("ln_fold", 0)  # the fold runs on family 7 only (its own test below)
         feats, offs = fe.extract_segments([torch.from_numpy(w) for w in wavs], cmn=True)
         uni = fe.extract(torch.from_numpy(_wav(75, 3, 32000)).to(DEV), cmn=True)
         got.append((feats.cpu().numpy(), uni.cpu().numpy()))
@@ -257,6 +259,33 @@ def test_direct_pos_conv_matches_grouped_gemm_and_oracle(sd_np, sd_t, layer):
         outs.append((feats.cpu(), offs))
     (a, offs), (b, _) = outs
     assert (a - b).abs().max().item() <= 2e-5
+    for i in (0, 1, 3):
+        with torch.no_grad():
+            if layer < 0:
+                ref = hubert_ref.s3prl_frontend(torch.from_numpy(wavs[i][None]), sd_t)[0]
+            else:
+                ref = hubert_ref.s3prl_upstream(torch.from_numpy(wavs[i][None]), sd_t)[layer][0]
+        assert (a[offs[i]:offs[i + 1]] - ref).abs().max().item() <= FEAT_ATOL, i
+
+
+@pytest.mark.parametrize("layer", [2, -1])
+def test_layernorm_fold_matches_kernels_and_oracle(sd_np, sd_t, layer):
+    """Option ln_fold 1 (default): the post-attention LayerNorm folded into the GEMMs — out_proj
+    emits per-row (mean, M2) partials, fc1 runs on the un-normalised rows with gamma in its
+    weights and applies (acc - mu colsum(W')) rstd + b + W beta, fc2 normalises its residual on
+    the fly — against ln_fold 0 (LayerNorm kernels) and the oracle, ragged batch included."""
+    lens = [100000, 700, 16000, 48000, 12345]
+    wavs = [_wav(90 + i, 1, n)[0] for i, n in enumerate(lens)]
+    outs = []
+    for lf in (1, 0):
+        fe = _frontend(sd_np, layer=layer, multilayer=layer < 0)
+        fe.set_option("ln_fold", lf)
+        assert fe.get_option("ln_fold") == lf
+        feats, offs = fe.extract_segments([torch.from_numpy(w) for w in wavs])
+        outs.append((feats.cpu(), offs))
+    (a, offs), (b, _) = outs
+    d = (a - b).abs().max().item()
+    assert d <= 5e-5, d
     for i in (0, 1, 3):
         with torch.no_grad():
             if layer < 0:

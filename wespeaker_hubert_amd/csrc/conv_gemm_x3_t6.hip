@@ -67,9 +67,66 @@ constexpr int kGEpiLd = 132;
 constexpr int kGEpiBytes = 8 * 32 * kGEpiLd * 4;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-template <int ACT, bool RB, bool RES>
+// LayerNorm fold (ConvGemmArgs::lnmode): mean and 1 / sqrt(var + eps) of row `row` from its
+// ln_parts (mean, M2) partials of 128 columns, combined in order (Chan et al.'s pairwise update;
+// every consumer of the row computes the same values).
+// Each lane computes one row (the wave's 64 rows); the epilogue fetches them by lane shuffle.
+constexpr int kLnMaxParts = 8;
+__device__ __forceinline__ void g_ln_row(const ConvGemmArgs& p, int row, float& mu, float& rstd) {
+  const float* s = p.ln_in + (size_t)row * p.ln_parts * 2;
+  float m = s[0], m2 = s[1];
+#pragma unroll
+  for (int k = 1; k < kLnMaxParts; ++k) {
+    if (k < p.ln_parts) {  // merge part k (128 values) into the first k parts (128 k values)
+      const float d = s[2 * k] - m;
+      m += d * (1.f / (float)(k + 1));
+      m2 += s[2 * k + 1] + d * d * (128.f * (float)k / (float)(k + 1));
+    }
+  }
+  mu = m;
+  rstd = 1.f / sqrtf(m2 / (128.f * (float)p.ln_parts) + p.ln_eps);
+}
+
+// (mean, M2) of the 128 values the 32 lanes of a half-wave hold (4 each) for R rows at once ->
+// lane 16 of the half (lanes 16 / 48): pairwise merges of equal counts, symmetric in the two
+// partners up to the last step (same result on both); the R rows' merge chains interleave
+template <int R>
+__device__ __forceinline__ void g_ln_pieces(float (&m)[R], float (&m2)[R]) {
+  float n = 4.f;
+  auto merge = [&](int i, float mo, float m2o) {
+    const float d = mo - m[i];
+    m[i] = 0.5f * (m[i] + mo);
+    m2[i] = (m2[i] + m2o) + d * d * (0.5f * n);
+  };
+#define WSP_DPP(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xF, 0xF, false))
+  // the first four steps inside rows of 16 lanes: quad xor 1, xor 2, then half-row / row mirrors
+  // (partners already hold equal values, so a mirror is the xor 4 / 8 exchange); then xor 16
+#pragma unroll
+  for (int i = 0; i < R; ++i) merge(i, WSP_DPP(m[i], 0xB1), WSP_DPP(m2[i], 0xB1));
+  n *= 2.f;
+#pragma unroll
+  for (int i = 0; i < R; ++i) merge(i, WSP_DPP(m[i], 0x4E), WSP_DPP(m2[i], 0x4E));
+  n *= 2.f;
+#pragma unroll
+  for (int i = 0; i < R; ++i) merge(i, WSP_DPP(m[i], 0x141), WSP_DPP(m2[i], 0x141));
+  n *= 2.f;
+#pragma unroll
+  for (int i = 0; i < R; ++i) merge(i, WSP_DPP(m[i], 0x140), WSP_DPP(m2[i], 0x140));
+  n *= 2.f;
+#undef WSP_DPP
+  // rows 1 / 3 of 16 lanes take row 0's / 2's value (row_bcast:15): lanes 16 and 48 end with the
+  // half-wave's statistics (the other rows keep their own)
+#define WSP_BC15(v) \
+  __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xA, 0xF, false))
+#pragma unroll
+  for (int i = 0; i < R; ++i) merge(i, WSP_BC15(m[i]), WSP_BC15(m2[i]));
+#undef WSP_BC15
+}
+
+template <int ACT, bool RB, bool RES, int LNM = 0>
 __device__ __forceinline__ void g_epilogue_rows(const ConvGemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0, int wm,
-                                                int wn, int wave, int lane, unsigned char* smem) {
+                                                int wn, int wave, int lane, unsigned char* smem, float lmu = 0.f,
+                                                float lrs = 1.f) {
   float* stg = reinterpret_cast<float*>(smem) + wave * 32 * kGEpiLd;
   const int c16 = lane & 15, q = lane >> 4;
   const int cl = 4 * (lane & 31);  // this lane's 4 columns within the wave's 128
@@ -77,10 +134,18 @@ __device__ __forceinline__ void g_epilogue_rows(const ConvGemmArgs& p, f32x4 (&a
   const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 sc = p.scale ? *reinterpret_cast<const f32x4*>(p.scale + col) : f32x4{1.f, 1.f, 1.f, 1.f};
   const f32x4 sh = p.scale ? *reinterpret_cast<const f32x4*>(p.shift + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 lcs{0.f, 0.f, 0.f, 0.f}, lg{1.f, 1.f, 1.f, 1.f}, lb{0.f, 0.f, 0.f, 0.f};
+  if constexpr ((LNM & 2) != 0) lcs = *reinterpret_cast<const f32x4*>(p.ln_cs + col);
+  if constexpr ((LNM & 4) != 0) {
+    lg = *reinterpret_cast<const f32x4*>(p.ln_g + col);
+    lb = *reinterpret_cast<const f32x4*>(p.ln_b + col);
+  }
+  const int lparts = p.N / 128, lpart = (n0 + wn * 128) / 128;  // lmu / lrs: row m0 + wm * 64 + lane
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out);
   const __amdgpu_buffer_rsrc_t rres = make_rsrc(RES ? p.res : p.out);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
+    float pm[(LNM & 1) ? 16 : 1], pm2[(LNM & 1) ? 16 : 1];  // LayerNorm pieces of the half's 16 rows
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
@@ -101,11 +166,22 @@ __device__ __forceinline__ void g_epilogue_rows(const ConvGemmArgs& p, f32x4 (&a
         const int ub = p.seg ? seg_of(p.seg, p.nseg, rowc) : rowc / p.T;
         rb = *reinterpret_cast<const f32x4*>(p.row_bias + (size_t)ub * p.N + col);
       }
+      float mu = 0.f, rstd = 1.f;
+      if constexpr ((LNM & 6) != 0) {  // row rl of this half: lane h * 32 + rl holds its statistics
+        auto rd = [](float v, int l) {
+          return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+        };
+        mu = lane < 32 ? rd(lmu, h * 32 + 2 * u) : rd(lmu, h * 32 + 2 * u + 1);
+        rstd = lane < 32 ? rd(lrs, h * 32 + 2 * u) : rd(lrs, h * 32 + 2 * u + 1);
+      }
       f32x4 y;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float v = x[e] + bv[e];
-        if constexpr (RES) v += rv[e];
+        float v;
+        if constexpr ((LNM & 2) != 0) v = (x[e] - mu * lcs[e]) * rstd + bv[e];
+        else v = x[e] + bv[e];
+        if constexpr ((LNM & 4) != 0) v += (rv[e] - mu) * rstd * lg[e] + lb[e];
+        else if constexpr (RES) v += rv[e];
         if constexpr (RB) v += rb[e];
         if constexpr (ACT == kActRelu) v = fmaxf(v, 0.f);
         else if constexpr (ACT == kActTanh) v = tanhf(v);
@@ -114,6 +190,23 @@ __device__ __forceinline__ void g_epilogue_rows(const ConvGemmArgs& p, f32x4 (&a
       }
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), ro, ok ? (row * p.ldo + col) * 4 : kOOB, 0,
                                              0);
+      if constexpr ((LNM & 1) != 0) {  // this lane's 4 values of the row: (mean, M2)
+        pm[u] = ((y[0] + y[1]) + (y[2] + y[3])) * 0.25f;
+        float q2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) q2 += (y[e] - pm[u]) * (y[e] - pm[u]);
+        pm2[u] = q2;
+      }
+    }
+    if constexpr ((LNM & 1) != 0) {  // merge the half-wave's 32 lanes per row; lanes 0 / 32 store
+      g_ln_pieces<16>(pm, pm2);
+      if ((lane & 31) == 16) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int row = m0 + wm * 64 + h * 32 + 2 * u + (lane >> 5);
+          if (row < p.M) *reinterpret_cast<float2*>(p.ln_out + ((size_t)row * lparts + lpart) * 2) = float2{pm[u], pm2[u]};
+        }
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next half overwrites
   }
@@ -215,7 +308,7 @@ __device__ __forceinline__ void g_epilogue_cs(const ConvGemmArgs& p, f32x4 (&acc
   }
 }
 
-template <int AM, bool CSK>
+template <int AM, bool CSK, int LNM = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, const __bf16* __restrict__ whi,
                                                       const __bf16* __restrict__ wlo) {
   using L = Lds<true, 16>;
@@ -359,6 +452,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
       }
   };
 
+  // LayerNorm fold: this lane's row statistics, loaded ahead of the first DMAs (their latency hides
+  // behind tile 0's) and held through the k-loop (2 registers)
+  float lmu = 0.f, lrs = 1.f;
+  if constexpr ((LNM & 6) != 0) g_ln_row(p, min(m0 + wm * 64 + lane, p.M - 1), lmu, lrs);
   dma(0, 0);
   dma(1, 1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0 landed (8 DMAs per k-tile and lane)
@@ -390,7 +487,14 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
     case kActGelu: g_epilogue_rows<kActGelu, RB, RES>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;    \
     default: g_epilogue_rows<kActNone, RB, RES>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;          \
   }
-  if constexpr (CSK) {  // SE column sums: own kernel instance (its epilogue's registers stay out of the others)
+  if constexpr (LNM != 0) {  // HuBERT LayerNorm fold instances (own kernels: the others keep their code)
+    if constexpr ((LNM & 5) != 0)
+      g_epilogue_rows<kActNone, false, true, LNM>(p, acc, m0, n0, wm, wn, wave, lane, smem, lmu, lrs);
+    else if (p.act == kActGelu)
+      g_epilogue_rows<kActGelu, false, false, LNM>(p, acc, m0, n0, wm, wn, wave, lane, smem, lmu, lrs);
+    else
+      g_epilogue_rows<kActNone, false, false, LNM>(p, acc, m0, n0, wm, wn, wave, lane, smem, lmu, lrs);
+  } else if constexpr (CSK) {  // SE column sums: own kernel instance (its epilogue's registers stay out of the others)
     switch (p.act) {
       case kActRelu: g_epilogue_cs<kActRelu>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;
       case kActTanh: g_epilogue_cs<kActTanh>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;
@@ -428,6 +532,24 @@ void t_g256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t
   // input offsets, and uniform batches with Ti == T); ragged iseg / Ti != T 1x1 GEMMs take AM 0.
   const bool dense = p.taps == 1 && p.pad == 0 && p.stride == 1 && !p.iseg && (p.seg || p.Ti == p.T);
   const int am = !uniform_ktiles(p) ? 2 : dense ? 1 : 0;
+  if (p.lnmode) {
+    // LayerNorm fold: 1 = emit (out_proj / fc2 on the residual), 2 = fold (qkv / fc1), 4 = residual
+    // normalised on the fly, 5 = both (fc2 / out_proj under the full fold)
+    WSP_CHECK(am == 1 && !p.colsum && !p.row_bias && !p.scale && p.N % 128 == 0 &&
+                  ((p.lnmode & 1) == 0 || (p.ln_out && p.res && p.act == kActNone)) &&
+                  ((p.lnmode & 6) == 0 || (p.ln_in && p.ln_parts >= 1 && p.ln_parts <= kLnMaxParts)) && ((p.lnmode & 2) == 0 || (p.ln_cs && !p.res)) &&
+                  ((p.lnmode & 4) == 0 || (p.ln_g && p.ln_b && p.res && p.act == kActNone)),
+              "conv_gemm_x3: LayerNorm fold needs a dense 1x1 GEMM and its operands");
+    switch (p.lnmode) {
+      case 1: hipLaunchKernelGGL((conv_gemm_g<1, false, 1>), dim3(nwg), dim3(512), lds, s, p, h, l); break;
+      case 2: hipLaunchKernelGGL((conv_gemm_g<1, false, 2>), dim3(nwg), dim3(512), lds, s, p, h, l); break;
+      case 4: hipLaunchKernelGGL((conv_gemm_g<1, false, 4>), dim3(nwg), dim3(512), lds, s, p, h, l); break;
+      case 5: hipLaunchKernelGGL((conv_gemm_g<1, false, 5>), dim3(nwg), dim3(512), lds, s, p, h, l); break;
+      default: WSP_CHECK(false, "conv_gemm_x3: lnmode must be 1, 2, 4 or 5");
+    }
+    WSP_HIP(hipGetLastError());
+    return;
+  }
   if (p.colsum && am == 1)
     hipLaunchKernelGGL((conv_gemm_g<1, true>), dim3(nwg), dim3(512), lds, s, p, h, l);
   else if (p.colsum && am == 0)

@@ -127,6 +127,29 @@ void Model::Impl::finalize_hubert() {
     L.fc2 = pack_conv(P(hp(p + "fc2.weight")), kHidden, kFfn, 1, P(hp(p + "fc2.bias")).data(), "");
     L.ln1_g = dev.upload(P(hp(p + "self_attn_layer_norm.weight")));
     L.ln1_b = dev.upload(P(hp(p + "self_attn_layer_norm.bias")));
+    {
+      // fc1 on LN1's input u: fc1(LN1(u)) = (u W'^T - mu cs) rstd + b + W beta, W' = W diag(gamma)
+      const auto& w1 = P(hp(p + "fc1.weight"));
+      const auto& b1 = P(hp(p + "fc1.bias"));
+      const auto& g1 = P(hp(p + "self_attn_layer_norm.weight"));
+      const auto& be1 = P(hp(p + "self_attn_layer_norm.bias"));
+      std::vector<float> wf(w1.size()), bf(kFfn), cs(kFfn);
+      for (int n = 0; n < kFfn; ++n) {
+        double bb = b1[n], c = 0.0;
+        for (int k = 0; k < kHidden; ++k) {
+          const float wv = w1[(size_t)n * kHidden + k];
+          wf[(size_t)n * kHidden + k] = wv * g1[k];
+          bb += (double)wv * be1[k];
+          const float x = wf[(size_t)n * kHidden + k];
+          const uint16_t h = f2bf(x);
+          c += (double)bf2f(h) + (double)bf2f(f2bf(x - bf2f(h)));
+        }
+        bf[n] = (float)bb;
+        cs[n] = (float)c;
+      }
+      L.fc1f = pack_conv(wf, kFfn, kHidden, 1, bf.data(), "");
+      L.fc1_cs = dev.upload(cs);
+    }
     L.ln2_g = dev.upload(P(hp(p + "final_layer_norm.weight")));
     L.ln2_b = dev.upload(P(hp(p + "final_layer_norm.bias")));
   }
@@ -217,9 +240,10 @@ size_t Model::Impl::hubert_ws_floats(const HubertPlan& pl, size_t* offs) const {
   const size_t sizes[] = {pl.maxA * kConvDim, pl.maxB * kConvDim, 2 * pl.maxStats,  // cnnA, cnnB, stats (f64)
                           M * kHidden,        M * kHidden,        M * 3 * kHidden,                     // x, x1, qkv
                           M * kHidden,        M * kFfn,                                                // ao, ffn / pos
-                          pl.offs.size()};                                                             // int32 offsets
+                          pl.offs.size(),                                                              // int32 offsets
+                          M * (kHidden / 128) * 2};                                                    // LN partials
   size_t o = 0;
-  for (int i = 0; i < 9; ++i) {
+  for (int i = 0; i < 10; ++i) {
     if (offs) offs[i] = o;
     o += (sizes[i] + 63) / 64 * 64;
   }
@@ -228,7 +252,7 @@ size_t Model::Impl::hubert_ws_floats(const HubertPlan& pl, size_t* offs) const {
 
 void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* feats, int cmn, float* ws,
                                  hipStream_t s) {
-  size_t off[9];
+  size_t off[10];
   hubert_ws_floats(pl, off);
   float* cnnA = ws + off[0];
   float* cnnB = ws + off[1];
@@ -241,6 +265,7 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
   float* cnn6 = qkv;  // [M][512] CNN output of the whole batch; qkv is first written by layer 0
   float* pc = ffn;  // the pos_conv output is consumed before fc1 writes
   int* dseg = reinterpret_cast<int*>(ws + off[8]);
+  float* lnst = ws + off[9];  // LN1 row statistics: [M][6] (mean, M2) of 128-column pieces
   // pageable source: the copy is staged before hipMemcpyAsync returns, so pl.offs may go away
   WSP_HIP(hipMemcpyAsync(dseg, pl.offs.data(), pl.offs.size() * sizeof(int), hipMemcpyHostToDevice, s));
   const int B = pl.B;
@@ -250,8 +275,18 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
 
   auto conv = [&](const char* tag, const ConvW& cw, const float* a, int lda, float* out, int ldo, int rows, int Ti,
                   int stride, int pad, int act, const float* res, bool bias, const int* oseg, const int* iseg, int nseg,
-                  int gcols = 0, int gcin = 0) {
+                  int gcols = 0, int gcin = 0, const ConvGemmArgs* lnf = nullptr) {
     ConvGemmArgs g{};
+    if (lnf) {  // LayerNorm fold fields
+      g.lnmode = lnf->lnmode;
+      g.ln_out = lnf->ln_out;
+      g.ln_in = lnf->ln_in;
+      g.ln_parts = lnf->ln_parts;
+      g.ln_cs = lnf->ln_cs;
+      g.ln_g = lnf->ln_g;
+      g.ln_b = lnf->ln_b;
+      g.ln_eps = lnf->ln_eps;
+    }
     g.a[0] = g.a[1] = g.a[2] = a;
     g.lda[0] = g.lda[1] = g.lda[2] = lda;
     g.cseg[0] = 0;
@@ -345,15 +380,39 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
          seg6, nullptr, B, kPosGout, kPosGin);
   }
   ln("h_ln", x, pc, x, M, kHidden, h_enc_g, h_enc_b, 0);
+  // LayerNorm fold: the GEMMs it touches run on tile family 7 (x3_variant 7, bf16x3)
+  const bool fold = ln_fold && precision == 1 && x3_variant == 7;
   for (int l = 0; l < kLayers; ++l) {
     const HLayer& L = h_layers[l];
     conv("h_qkv", L.qkv, x, kHidden, qkv, 3 * kHidden, M, M, 1, 0, kActNone, nullptr, true, nullptr, nullptr, 0);
     run("h_attn", 4.0 * B * kHeads * (double)pl.maxT6 * pl.maxT6 * (kHidden / kHeads), s,
         [&] { launch_attn(qkv, 3 * kHidden, ao, kHidden, B, pl.maxT6, kHeads, kHidden / kHeads, s, seg6, attn_pipe); });
-    conv("h_out_proj", L.out, ao, kHidden, x1, kHidden, M, M, 1, 0, kActNone, x, true, nullptr, nullptr, 0);
-    ln("h_ln", x1, nullptr, x, M, kHidden, L.ln1_g, L.ln1_b, -1);
-    conv("h_fc1", L.fc1, x, kHidden, ffn, kFfn, M, M, 1, 0, kActGelu, nullptr, true, nullptr, nullptr, 0);
-    conv("h_fc2", L.fc2, ffn, kFfn, x1, kHidden, M, M, 1, 0, kActNone, x, true, nullptr, nullptr, 0);
+    if (fold) {
+      // LN1 folded: out_proj emits x1's row statistics, fc1 runs on x1 with gamma1 / beta1 in its
+      // weights, fc2 normalises its residual x1 on the fly (in place: each element is read by the
+      // lane that then overwrites it)
+      ConvGemmArgs f{};
+      f.ln_parts = kHidden / 128;
+      f.ln_eps = 1e-5f;
+      f.lnmode = 1;
+      f.ln_out = lnst;
+      conv("h_out_proj", L.out, ao, kHidden, x1, kHidden, M, M, 1, 0, kActNone, x, true, nullptr, nullptr, 0, 0, 0, &f);
+      f.lnmode = 2;
+      f.ln_out = nullptr;
+      f.ln_in = lnst;
+      f.ln_cs = L.fc1_cs;
+      conv("h_fc1", L.fc1f, x1, kHidden, ffn, kFfn, M, M, 1, 0, kActGelu, nullptr, true, nullptr, nullptr, 0, 0, 0, &f);
+      f.lnmode = 4;
+      f.ln_cs = nullptr;
+      f.ln_g = L.ln1_g;
+      f.ln_b = L.ln1_b;
+      conv("h_fc2", L.fc2, ffn, kFfn, x1, kHidden, M, M, 1, 0, kActNone, x1, true, nullptr, nullptr, 0, 0, 0, &f);
+    } else {
+      conv("h_out_proj", L.out, ao, kHidden, x1, kHidden, M, M, 1, 0, kActNone, x, true, nullptr, nullptr, 0);
+      ln("h_ln", x1, nullptr, x, M, kHidden, L.ln1_g, L.ln1_b, -1);
+      conv("h_fc1", L.fc1, x, kHidden, ffn, kFfn, M, M, 1, 0, kActGelu, nullptr, true, nullptr, nullptr, 0);
+      conv("h_fc2", L.fc2, ffn, kFfn, x1, kHidden, M, M, 1, 0, kActNone, x, true, nullptr, nullptr, 0);
+    }
     ln("h_ln", x1, nullptr, x, M, kHidden, L.ln2_g, L.ln2_b, l + 1);
   }
   if (cmn) run("h_cmn", 0, s, [&] { launch_cmn_rows(feats, B, 0, kHidden, s, fseg); });

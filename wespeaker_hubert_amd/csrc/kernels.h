@@ -64,6 +64,20 @@ struct ConvGemmArgs {
   // utterance of the block's first row, 1 = the next); conv_gemm_colsum_mean()
   // turns them into per-utterance means (the SE squeeze, ecapa_tdnn.py:118).
   double* colsum;
+  // HuBERT LayerNorm fold (x3 tile family 7, dense 1x1 GEMMs only; conv_gemm_x3_t6.hip).
+  // lnmode bits: 1 = emit the row statistics of the output y as (mean, M2) partials of its
+  // 128-column pieces, ln_out [M][N / 128][2]; 2 = fold: y = (acc - mu ln_cs[n]) rstd + bias
+  // (A = the un-normalised rows, W pre-scaled by gamma, bias = b + W beta); 4 = the residual
+  // is normalised on the fly: res = (res - mu) rstd ln_g + ln_b.  Modes 2 / 4 read mu, rstd
+  // from ln_in [M][ln_parts][2] (partials of 128 columns, ln_parts x 128 = the normalised width).
+  int lnmode;
+  float* ln_out;
+  const float* ln_in;
+  int ln_parts;
+  const float* ln_cs;
+  const float* ln_g;
+  const float* ln_b;
+  float ln_eps;
 };
 
 // Fills the 1-D defaults (stride 1, Ti = T) of a zero-initialised ConvGemmArgs.

@@ -202,12 +202,17 @@ struct Model::Impl {
   struct HLayer {
     ConvW qkv, out, fc1, fc2;
     float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
+    // LayerNorm fold (option ln_fold): fc1 on the un-normalised rows with gamma1 folded into W
+    // and W beta1 into the bias; fc1_cs[n] = sum_c W'[n][c] (of the bf16 hi + lo images)
+    ConvW fc1f;
+    float* fc1_cs = nullptr;
   };
   std::vector<HLayer> h_layers;
   std::vector<float> h_fw;  // featurizer weight per hidden state
   int h_layer_sel = -1;     // s3prl `layer` (-1: softmax-weighted sum of all 13)
   int attn_pipe = 1;        // attn.hip: 1 = persistent pipelined kernel, 0 = one block per (utterance, head)
   int pos_conv = 1;         // HuBERT pos_conv: 1 = direct grouped conv (pos_conv.hip), 0 = grouped implicit GEMM
+  int ln_fold = 1;          // HuBERT: 1 = the post-attention LayerNorm folded into out_proj / fc1 / fc2 (x3_variant 7)
   void build_hubert_params();
   void finalize_hubert();
   int hubert_cnn_frames(int N, int upto) const;
