@@ -172,6 +172,10 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *                  conv (pos_conv.hip: one block per 256 frames x group, input patch split into
  *                  bf16 hi / lo once in LDS; default), 0 = the grouped implicit GEMM (48 of 64
  *                  padded columns per group); equal up to fp32 rounding
+ *   "ln_fold"      HuBERT front end, x3_variant 7: 1 = the post-attention LayerNorm folded into
+ *                  the GEMMs (out_proj emits per-row mean / M2 partials, fc1 runs on the
+ *                  un-normalised rows with gamma in W, fc2 normalises its residual on the fly;
+ *                  12 fewer launches per forward, measured neutral), 0 = LayerNorm kernels (default)
  *   "layer"        HuBERT front end only, before finalize: -1 = weighted sum of all
  *                  hidden states (default), k = hidden state k alone (s3prl.py:84-87)
  * Deprecated (accepted, mapped to the shipped kernels since r3 pruned the others):

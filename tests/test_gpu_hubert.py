@@ -270,7 +270,7 @@ def test_direct_pos_conv_matches_grouped_gemm_and_oracle(sd_np, sd_t, layer):
 
 @pytest.mark.parametrize("layer", [2, -1])
 def test_layernorm_fold_matches_kernels_and_oracle(sd_np, sd_t, layer):
-    """Option ln_fold 1 (default): the post-attention LayerNorm folded into the GEMMs — out_proj
+    """Option ln_fold 1: the post-attention LayerNorm folded into the GEMMs — out_proj
     emits per-row (mean, M2) partials, fc1 runs on the un-normalised rows with gamma in its
     weights and applies (acc - mu colsum(W')) rstd + b + W beta, fc2 normalises its residual on
     the fly — against ln_fold 0 (LayerNorm kernels) and the oracle, ragged batch included."""

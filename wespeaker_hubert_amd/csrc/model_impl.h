@@ -212,7 +212,9 @@ struct Model::Impl {
   int h_layer_sel = -1;     // s3prl `layer` (-1: softmax-weighted sum of all 13)
   int attn_pipe = 1;        // attn.hip: 1 = persistent pipelined kernel, 0 = one block per (utterance, head)
   int pos_conv = 1;         // HuBERT pos_conv: 1 = direct grouped conv (pos_conv.hip), 0 = grouped implicit GEMM
-  int ln_fold = 1;          // HuBERT: 1 = the post-attention LayerNorm folded into out_proj / fc1 / fc2 (x3_variant 7)
+  // HuBERT: 1 = the post-attention LayerNorm folded into out_proj / fc1 / fc2 (x3_variant 7); measured
+  // neutral on C4 (A/B 4 234 / 4 223 vs 4 233 / 4 232 emb/s, profiles/r5g_ln_fold.txt): default off
+  int ln_fold = 0;
   void build_hubert_params();
   void finalize_hubert();
   int hubert_cnn_frames(int N, int upto) const;
