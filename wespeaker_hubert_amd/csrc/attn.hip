@@ -213,7 +213,8 @@ __global__ __launch_bounds__(512, 2) void attn_kernel(const float* __restrict__ 
 // one half out of LDS, the next half's K / V rows (the next item's first half at an
 // item's end) are already in flight to registers, then written into the other of two
 // LDS buffers — so the staging that the one-block-per-CU kernel above exposes per
-// (utterance, head) overlaps the MFMAs.  Same per-chunk arithmetic and chunk order.
+// (utterance, head) overlaps the MFMAs.  Same chunk order; r5: the softmax in the log2 domain
+// with a lazily raised maximum (equal up to fp32 rounding; h_attn -8 %, VALU-bound chunk loop).
 constexpr int kKH = 128;                            // keys per staged half
 constexpr int kVRowH = 264;                         // V^T row stride: 128 keys + 8 B (2-dword bank shift per row)
 constexpr int kKPlaneH = kKH * kDh * 2;             // 16 KB per K plane
@@ -315,10 +316,11 @@ __global__ __launch_bounds__(512, 2) void attn_pipe_kernel(const float* __restri
     const bool wave_live = q0 + wave * 32 < T;  // wave-uniform
     const float* base = base_of(it);
     if (hf == 0 && wave_live) {
-      // Q^T fragments (B operand of S^T = K Q^T), pre-scaled by 1/sqrt(dh) = 1/8; issued
+      // Q^T fragments (B operand of S^T = K Q^T), pre-scaled by log2(e) / sqrt(dh): the scores
+      // come out in the log2 domain, so the softmax takes one v_exp_f32 per score (r5); issued
       // before the next half's loads, so waiting for them does not wait for those
       const float* qr = base + (size_t)min(q, T - 1) * ldq + head * kDh + 8 * hh;
-      const float sc = q < T ? scale : 0.f;
+      const float sc = q < T ? scale * 1.4426950408889634f : 0.f;
 #pragma unroll
       for (int s = 0; s < 4; ++s)
         split8(*reinterpret_cast<const f32x4*>(qr + 16 * s) * sc, *reinterpret_cast<const f32x4*>(qr + 16 * s + 4) * sc,
@@ -352,30 +354,40 @@ __global__ __launch_bounds__(512, 2) void attn_pipe_kernel(const float* __restri
           st = mma3(*reinterpret_cast<const bf16x8*>(kh_s + ka), *reinterpret_cast<const bf16x8*>(kl_s + ka), qh[s],
                     ql[s], st);
         }
+        // online softmax in the log2 domain with a lazy maximum (r5): the running max m moves
+        // only when a score exceeds it by more than 8 (p <= 2^8 then; l <= 2^8 x keys), so the
+        // 32-register rescale of O runs on the few chunks that raise the max, not on every
+        // chunk; masks only in the utterance's last, partial chunk
+        const bool part = c * 32 + 32 > nk;  // wave-uniform
         float cmax = -FLT_MAX;
+        if (part) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int kk = c * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if (kk >= nk) st[e] = -FLT_MAX;
-          cmax = fmaxf(cmax, st[e]);
+          for (int e = 0; e < 16; ++e) {
+            const int kk = c * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+            if (kk >= nk) st[e] = -FLT_MAX;
+          }
         }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) cmax = fmaxf(cmax, st[e]);
         cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-        const float mn = fmaxf(m, cmax);
-        const float corr = __expf(m - mn);
+        if (__any(cmax > m + 8.f)) {  // wave-uniform
+          const float mn = cmax > m + 8.f ? cmax : m;
+          const float corr = __builtin_amdgcn_exp2f(m - mn);
+          l *= corr;
+          m = mn;
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) o[t][e] *= corr;
+        }
         float ls = 0.f;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int kk = c * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          const float pe = kk < nk ? __expf(st[e] - mn) : 0.f;
+          const float pe = __builtin_amdgcn_exp2f(st[e] - m);  // masked scores: exp2(-huge) = 0
           st[e] = pe;
           ls += pe;
         }
-        l = l * corr + ls;
-        m = mn;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) o[t][e] *= corr;
+        l += ls;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           bf16x8 ph, pl;
