@@ -5,7 +5,7 @@
 // accumulation) as conv_gemm_x3.
 //
 // The grouped implicit GEMM (conv_gemm_x3's gcols path) pads every group's 48 output columns to
-// 64 (a third of its MFMAs multiply zeros), re-stages the same input rows for each of the 128
+// 64 (a quarter of its MFMAs multiply zeros), re-stages the same input rows for each of the 128
 // taps, and splits fp32 A into hi / lo on every k-tile.  Here one block owns 256 output frames of
 // one utterance and one group:
 //   * the input patch — frames t0 - 64 .. t0 + 319 (zeros outside the utterance) x the group's 48
