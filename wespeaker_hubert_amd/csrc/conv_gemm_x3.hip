@@ -62,19 +62,12 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
               "conv_gemm_x3: column sums need a uniform batch with T >= block rows and no row bias");
   }
   WSP_CHECK(p.Kp % 64 == 0, "conv_gemm_x3: packed K must be a multiple of 64");
-  WSP_CHECK((variant >= 3 && variant <= 7) || variant == 9, "conv_gemm_x3: tile family must be 3, 4, 5, 6, 7 or 9");
+  WSP_CHECK(variant >= 3 && variant <= 7, "conv_gemm_x3: tile family must be 3, 4, 5, 6 or 7");
   const __bf16* h = static_cast<const __bf16*>(whi);
   const __bf16* l = static_cast<const __bf16*>(wlo);
   x3::TileFn f;
-  WSP_CHECK(!p.lnmode || ((variant == 7 || variant == 9) && x3::g256_supported(p)),
+  WSP_CHECK(!p.lnmode || (variant == 7 && x3::g256_supported(p)),
             "conv_gemm_x3: the LayerNorm fold runs on tile family 7 only");
-  if (variant == 9 && x3::q256_supported(p)) {
-    // variant 9 (r5): family 7 on 16 waves of 64 x 64 (conv_gemm_x3_t7.hip), bit-identical; the
-    // operands it does not take (column sums, LayerNorm fold, k-tiles straddling taps) run on 7
-    x3::t_q256(p, h, l, s);
-    return;
-  }
-  if (variant == 9) variant = 7;
   if (variant == 7 && x3::g256_supported(p)) {
     // variant 7 (r4): the 256 x 256 16x16x32 tile with every operand staged by LDS-DMA and the
     // fp32 A split at fragment time (conv_gemm_x3_t6.hip); bit-identical to 6, which serves
