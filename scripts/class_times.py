@@ -36,7 +36,8 @@ def main():
     B = a.batch or (128 if resnet_like else 256)
     w = bench.build_workload(args, a.arch, B, 0, dev)
     handles = [h for h in (w.get("fe"), w["model"]) if h is not None]
-    tags = bench.HEAD_TAGS + bench.HUBERT_TAGS + tuple(f"h_cnn.c{i}" for i in range(1, 7))
+    tags = bench.HEAD_TAGS + bench.HUBERT_TAGS + tuple(f"h_cnn.c{i}" for i in range(1, 7)) + \
+        tuple(f"res_tail.L{i}" for i in range(1, 5))
     out = {}
     for h in handles:
         r = bench.standalone_pass(w, h, tags, steps=a.steps)
