@@ -15,6 +15,7 @@
 #include <vector>
 #include "../wespeaker_hubert_amd/csrc/conv_gemm_x3_t5.hip"
 #include "../wespeaker_hubert_amd/csrc/conv_gemm_x3_t6.hip"
+#include "../wespeaker_hubert_amd/csrc/conv_gemm_x3_t7.hip"
 namespace wsp { namespace x3 {
 void t_4x2_2x4_sw1(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t) { std::abort(); }
 } }
@@ -155,7 +156,10 @@ void run(const Case& c, int v, float* out, double* cs, hipStream_t s) {
   q.out = out;
   q.colsum = cs;
   if (v == 6) x3::t_4x2_2x4_mf16(q, c.whi, c.wlo, s);
-  else {
+  else if (v == 8) {  // family 7, persistent form
+    if (!x3::gp256_supported(q)) { std::fprintf(stderr, "%s: the persistent form does not take these operands\n", c.name.c_str()); std::exit(2); }
+    x3::t_gp256(q, c.whi, c.wlo, s);
+  } else {
     if (!x3::g256_supported(q)) { std::fprintf(stderr, "%s: family %d does not take these operands\n", c.name.c_str(), v); std::exit(2); }
     x3::t_g256(q, c.whi, c.wlo, s);
   }
