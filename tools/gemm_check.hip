@@ -3,8 +3,8 @@
 // operand shapes the models launch, plus the operand forms only tests reach (ragged row bias,
 // 1x1 with Ti != T).  Family 7 must equal family 6 bit for bit (outputs and SE column sums); then
 // interleaved timing rounds.  (r5's family 8, a ping-pong k-loop, and family 9, family 7 on 16 waves
-// of 64 x 64 or 8 waves of 32 x 256, were measured with this tool and pruned:
-// profiles/r5a_gemm_check.txt, r5m_gemm_family9.txt.)
+// of 64 x 64 or 8 waves of 32 x 256, and a persistent family 7, were measured with this tool and
+// pruned: profiles/r5a_gemm_check.txt, r5m_gemm_family9.txt, r5p_gemm_persistent.txt.)
 //   gemm_check [case|all] [reps] [variants, e.g. 67]
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -15,7 +15,6 @@
 #include <vector>
 #include "../wespeaker_hubert_amd/csrc/conv_gemm_x3_t5.hip"
 #include "../wespeaker_hubert_amd/csrc/conv_gemm_x3_t6.hip"
-#include "../wespeaker_hubert_amd/csrc/conv_gemm_x3_t7.hip"
 namespace wsp { namespace x3 {
 void t_4x2_2x4_sw1(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t) { std::abort(); }
 } }
@@ -156,10 +155,7 @@ void run(const Case& c, int v, float* out, double* cs, hipStream_t s) {
   q.out = out;
   q.colsum = cs;
   if (v == 6) x3::t_4x2_2x4_mf16(q, c.whi, c.wlo, s);
-  else if (v == 8) {  // family 7, persistent form
-    if (!x3::gp256_supported(q)) { std::fprintf(stderr, "%s: the persistent form does not take these operands\n", c.name.c_str()); std::exit(2); }
-    x3::t_gp256(q, c.whi, c.wlo, s);
-  } else {
+  else {
     if (!x3::g256_supported(q)) { std::fprintf(stderr, "%s: family %d does not take these operands\n", c.name.c_str(), v); std::exit(2); }
     x3::t_g256(q, c.whi, c.wlo, s);
   }
