@@ -201,7 +201,7 @@ HubertPlan Model::Impl::hubert_plan(int B, const int* lens) const {
     pl.chunks.push_back({b0, b1});
     b0 = b1;
   }
-  // offsets: global [seg6 | fseg], then per chunk [wseg | seg0 .. seg6] relative to the chunk
+  // offsets: global [seg6 | fseg | seg3 | seg4 | seg5], then per chunk [wseg | seg0 .. seg6] relative to the chunk
   auto prefix = [&](const std::vector<int>& v, int lo, int hi) {
     long long acc = 0;
     pl.offs.push_back(0);
@@ -214,6 +214,11 @@ HubertPlan Model::Impl::hubert_plan(int B, const int* lens) const {
   };
   pl.M = prefix(T[6], 0, B);
   pl.Mout = prefix(Tout, 0, B);
+  // CNN layers 4..6 run once over the whole batch when the level-3 rows fit a 2 GiB operand (r5:
+  // the per-chunk launches of these short layers filled 112-446 of the 256 CUs)
+  pl.M3 = prefix(T[3], 0, B);
+  pl.M4 = prefix(T[4], 0, B);
+  pl.M5 = prefix(T[5], 0, B);
   std::vector<int> lv(lens, lens + B);
   for (auto& c : pl.chunks) {
     c.off = pl.offs.size();
@@ -221,6 +226,8 @@ HubertPlan Model::Impl::hubert_plan(int B, const int* lens) const {
     for (int k = 0; k < 7; ++k) c.rows[k] = prefix(T[k], c.b0, c.b1);
     c.row6 = 0;
     for (int b = 0; b < c.b0; ++b) c.row6 += T[6][b];
+    c.row3 = 0;
+    for (int b = 0; b < c.b0; ++b) c.row3 += T[3][b];
     c.sample0 = 0;
     for (int b = 0; b < c.b0; ++b) c.sample0 += lens[b];
     c.maxT0 = *std::max_element(T[0].begin() + c.b0, T[0].begin() + c.b1);
@@ -230,6 +237,10 @@ HubertPlan Model::Impl::hubert_plan(int B, const int* lens) const {
     pl.maxStats = std::max(pl.maxStats, hubert_conv0_stats_doubles(c.b1 - c.b0, c.maxT0));
   }
   pl.maxT6 = *std::max_element(T[6].begin(), T[6].end());
+  // layers 4..6 batch-wide: more than one chunk, level-3 rows within a 2 GiB operand, and the
+  // chunk buffers (free after the chunk loop) large enough for the level-4 / level-5 rows
+  pl.tail_batch = pl.chunks.size() > 1 && pl.M3 * kConvDim * sizeof(float) < ((size_t)1 << 31) / 8 * 7 &&
+                  pl.M4 <= pl.maxA && pl.M5 <= pl.maxB;
   WSP_CHECK(pl.M * kFfn * sizeof(float) < ((size_t)1 << 31) - 64,
             "HuBERT batch too large for one call (frames * 3072 floats must stay below 2 GiB)");
   return pl;
@@ -241,9 +252,10 @@ size_t Model::Impl::hubert_ws_floats(const HubertPlan& pl, size_t* offs) const {
                           M * kHidden,        M * kHidden,        M * 3 * kHidden,                     // x, x1, qkv
                           M * kHidden,        M * kFfn,                                                // ao, ffn / pos
                           pl.offs.size(),                                                              // int32 offsets
-                          M * (kHidden / 128) * 2};                                                    // LN partials
+                          M * (kHidden / 128) * 2,                                                     // LN partials
+                          pl.tail_batch ? pl.M3 * kConvDim : 0};                                       // level-3 rows
   size_t o = 0;
-  for (int i = 0; i < 10; ++i) {
+  for (int i = 0; i < 11; ++i) {
     if (offs) offs[i] = o;
     o += (sizes[i] + 63) / 64 * 64;
   }
@@ -252,7 +264,7 @@ size_t Model::Impl::hubert_ws_floats(const HubertPlan& pl, size_t* offs) const {
 
 void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* feats, int cmn, float* ws,
                                  hipStream_t s) {
-  size_t off[10];
+  size_t off[11];
   hubert_ws_floats(pl, off);
   float* cnnA = ws + off[0];
   float* cnnB = ws + off[1];
@@ -272,6 +284,10 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
   const int M = (int)pl.M;
   const int* seg6 = dseg;           // [B+1] hidden-state rows per utterance
   const int* fseg = dseg + B + 1;   // [B+1] output feature rows per utterance
+  const int* gseg3 = dseg + 2 * (B + 1);  // [B+1] batch-wide rows of conv levels 3, 4, 5
+  const int* gseg4 = dseg + 3 * (B + 1);
+  const int* gseg5 = dseg + 4 * (B + 1);
+  float* cnn3 = ws + off[10];       // tail_batch: [M3][512] level-3 rows of the whole batch
 
   auto conv = [&](const char* tag, const ConvW& cw, const float* a, int lda, float* out, int ldo, int rows, int Ti,
                   int stride, int pad, int act, const float* res, bool bias, const int* oseg, const int* iseg, int nseg,
@@ -355,12 +371,26 @@ void Model::Impl::forward_hubert(const float* wav, const HubertPlan& pl, float* 
     float* dst = cnnB;
     // profiling sub-classes per layer: h_cnn.c<i>
     static const char* kCnn[7] = {"", "h_cnn.c1", "h_cnn.c2", "h_cnn.c3", "h_cnn.c4", "h_cnn.c5", "h_cnn.c6"};
-    for (int i = 1; i < 7; ++i) {
-      // the last layer writes this chunk's rows of the whole batch's CNN output (cnn6)
-      float* o = i == 6 ? cnn6 + c.row6 * kConvDim : dst;
+    const int last = pl.tail_batch ? 3 : 6;
+    for (int i = 1; i <= last; ++i) {
+      // the last layer writes this chunk's rows of the whole batch's level-`last` output
+      float* o = i == 6 ? cnn6 + c.row6 * kConvDim : i == last ? cnn3 + c.row3 * kConvDim : dst;
       conv(kCnn[i], h_conv[i], src, kConvDim, o, kConvDim, (int)c.rows[i], (int)c.rows[i - 1], kConvS[i], 0,
            kActGelu, nullptr, false, lvl(i), lvl(i - 1), nb);
       std::swap(src, dst);
+    }
+  }
+  if (pl.tail_batch) {
+    // layers 4..6 once over the whole batch (the chunk buffers are free now): cnn3 -> cnnA -> cnnB -> cnn6
+    static const char* kCnnT[3] = {"h_cnn.c4", "h_cnn.c5", "h_cnn.c6"};
+    const int* gs[4] = {gseg3, gseg4, gseg5, seg6};
+    const float* in = cnn3;
+    float* outs[3] = {cnnA, cnnB, cnn6};
+    const size_t rows[4] = {pl.M3, pl.M4, pl.M5, pl.M};
+    for (int i = 4; i < 7; ++i) {
+      conv(kCnnT[i - 4], h_conv[i], in, kConvDim, outs[i - 4], kConvDim, (int)rows[i - 3], (int)rows[i - 4], kConvS[i],
+           0, kActGelu, nullptr, false, gs[i - 3], gs[i - 4], B);
+      in = outs[i - 4];
     }
   }
   // LayerNorm + feature projection once over every chunk's rows (row-local: the same results as

@@ -90,11 +90,16 @@ struct HubertChunk {
   size_t off = 0;       // index of this chunk's tables in HubertPlan::offs
   size_t rows[7] = {};  // conv-level frame rows of the chunk
   size_t samples = 0, sample0 = 0, row6 = 0;
+  size_t row3 = 0;  // the chunk's first row in the batch-wide level-3 rows (cnn_tail_batch)
   int maxT0 = 0;
 };
 struct HubertPlan {
   int B = 0;
   size_t M = 0, Mout = 0, maxA = 0, maxB = 0;
+  // batch-wide rows of conv levels 3..5 and whether CNN layers 4..6 run once over the batch
+  // (their global offsets follow seg6 | fseg in offs as seg3 | seg4 | seg5)
+  size_t M3 = 0, M4 = 0, M5 = 0;
+  bool tail_batch = false;
   int maxChunk = 0, maxT6 = 0;
   size_t maxStats = 0;  // doubles of conv0 partial moments (hubert_conv0_stats_doubles) of the largest chunk
   std::vector<HubertChunk> chunks;
