@@ -122,6 +122,10 @@ struct SmallLinearArgs {
   int ldo;
   int R, K, N;
   int act;
+  // optional scratch for long K (>= 4096): the k range splits over blocks (split-K partials
+  // [KS][R][N], summed in slice order by a second pass); null = one pass, 4 rows per block
+  float* scratch = nullptr;
+  size_t scratch_floats = 0;
 };
 void launch_small_linear(const SmallLinearArgs& p, hipStream_t s);
 

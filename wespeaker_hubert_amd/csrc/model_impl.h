@@ -753,13 +753,17 @@ struct Model::Impl {
       run("tstp_head", 0, s, [&] {
         launch_frame_stats(x, Ci, nb * Fi, Ti, Ci, pooled, 2 * Ci, 1, Ci, s);
         float* e_out = embed + (size_t)b0 * embed_dim;
+        // split-K partials of seg_1 (K = F/8 x 2 x C) in the free second conv1 buffer
+        const size_t sk = off[4] - off[3];
         if (two_emb) {
           // relu(seg_1(stats)) into the free conv1 buffer, then the folded seg_bn_1 + seg_2
-          launch_small_linear({pooled, Fi * 2 * Ci, seg1.wt, seg1.bias, Y1, embed_dim, nb, Fi * 2 * Ci, embed_dim, 1},
+          launch_small_linear({pooled, Fi * 2 * Ci, seg1.wt, seg1.bias, Y1, embed_dim, nb, Fi * 2 * Ci, embed_dim, 1,
+                               Y2, sk},
                               s);
           launch_small_linear({Y1, embed_dim, seg2.wt, seg2.bias, e_out, embed_dim, nb, embed_dim, embed_dim, 0}, s);
         } else {
-          launch_small_linear({pooled, Fi * 2 * Ci, seg1.wt, seg1.bias, e_out, embed_dim, nb, Fi * 2 * Ci, embed_dim, 0},
+          launch_small_linear({pooled, Fi * 2 * Ci, seg1.wt, seg1.bias, e_out, embed_dim, nb, Fi * 2 * Ci, embed_dim, 0,
+                               Y2, sk},
                               s);
         }
       });
@@ -938,8 +942,9 @@ struct Model::Impl {
       gemm("asp_linear2", asp2, att, 128, logit, CF, nb * Ti, Ti, 1, 0, kActNone, s);
       run("asp_pool_head", 0, s, [&] {
         launch_astp_pool(logit, Xt, nb, Ti, CF, pooled, s, nullptr, 1e-5f);
+        // split-K partials in the free conv1 buffer
         launch_small_linear({pooled, 2 * CF, simam_head.wt, simam_head.bias, embed + (size_t)b0 * embed_dim,
-                             embed_dim, nb, 2 * CF, embed_dim, 0},
+                             embed_dim, nb, 2 * CF, embed_dim, 0, Y1, off[3] - off[2]},
                             s);
       });
     }

@@ -68,10 +68,75 @@ __global__ __launch_bounds__(64 * kSW) void small_linear_kernel(const SmallLinea
     p.out[(long)(r0 + r) * p.ldo + n] = y;
   }
 }
+
+// Split-K form for long K (r5; the ResNet / SimAM heads, K = F/8 x 2 x C = 10-20k): block
+// (row block of 16, 64 columns, k slice) -> partial sums part[slice][row][col]; the 16 waves split
+// the slice and reduce through LDS in wave order.  The one-pass kernel above ran 64 blocks, each
+// row block re-reading the whole weight matrix (C3: 0.29 ms per head launch).
+constexpr int kSKR = 16;  // rows per split-K block
+__global__ __launch_bounds__(64 * kSW) void small_linear_splitk_kernel(const SmallLinearArgs p, int kslice) {
+  __shared__ float part[kSW][kSKR][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int n = blockIdx.y * 64 + lane;
+  const int r0 = blockIdx.x * kSKR;
+  const int ks = blockIdx.z;
+  const int kb = ks * kslice, ke = min(p.K, kb + kslice);
+  const int kq = (ke - kb + kSW - 1) / kSW;
+  const int k0 = kb + wave * kq, k1 = min(ke, k0 + kq);
+  float acc[kSKR];
+#pragma unroll
+  for (int r = 0; r < kSKR; ++r) acc[r] = 0.f;
+  if (n < p.N) {
+    const float* w = p.wt + n;
+    for (int k = k0; k < k1; ++k) {
+      const float wk = w[(long)k * p.N];
+#pragma unroll
+      for (int r = 0; r < kSKR; ++r) acc[r] = fmaf(p.in[(long)min(r0 + r, p.R - 1) * p.ldin + k], wk, acc[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kSKR; ++r) part[wave][r][lane] = acc[r];
+  __syncthreads();
+  // waves 0 .. kSKR - 1: wave r sums row r over the 16 waves in order
+  if (wave < kSKR && n < p.N && r0 + wave < p.R) {
+    float y = 0.f;
+#pragma unroll
+    for (int w = 0; w < kSW; ++w) y += part[w][wave][lane];
+    p.scratch[((size_t)ks * p.R + r0 + wave) * p.N + n] = y;
+  }
+}
+
+__global__ __launch_bounds__(256) void small_linear_reduce_kernel(const SmallLinearArgs p, int nks) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.R * p.N) return;
+  const int r = i / p.N, n = i - r * p.N;
+  float y = 0.f;
+  for (int ks = 0; ks < nks; ++ks) y += p.scratch[(size_t)ks * p.R * p.N + i];
+  y += p.bias ? p.bias[n] : 0.f;
+  if (p.act == 1) y = fmaxf(y, 0.f);
+  else if (p.act == 2) y = tanhf(y);
+  else if (p.act == 3) y = 1.f / (1.f + expf(-y));
+  p.out[(long)r * p.ldo + n] = y;
+}
 }  // namespace
 
 void launch_small_linear(const SmallLinearArgs& p, hipStream_t s) {
   if (p.R == 0) return;
+  const int rb = ceil_div(p.R, kSKR), nb = ceil_div(p.N, 64);
+  // 32 k slices (of >= 256): the slicing depends on K alone, so every row sums its products in
+  // the same order whatever the batch (rows of a batch equal their batch-of-one results)
+  if (p.scratch && p.K >= 4096) {
+    const int kslice = std::max(256, (ceil_div(p.K, 32) + 63) / 64 * 64);
+    const int nks = ceil_div(p.K, kslice);
+    if ((size_t)nks * p.R * p.N <= p.scratch_floats) {
+      hipLaunchKernelGGL(small_linear_splitk_kernel, dim3(rb, nb, nks), dim3(64 * kSW), 0, s, p, kslice);
+      WSP_HIP(hipGetLastError());
+      hipLaunchKernelGGL(small_linear_reduce_kernel, dim3(ceil_div(p.R * p.N, 256)), dim3(256), 0, s, p, nks);
+      WSP_HIP(hipGetLastError());
+      return;
+    }
+  }
   dim3 grid(ceil_div(p.R, kRB), ceil_div(p.N, 64));
   hipLaunchKernelGGL(small_linear_kernel, grid, dim3(64 * kSW), 0, s, p);
   WSP_HIP(hipGetLastError());
