@@ -17,7 +17,8 @@
 // latency-bound.
 //
 // Layout: one workgroup (16 waves) = one utterance; wave w takes frames
-// w, w+16, ...  Each wave owns a 256-entry complex f64 LDS buffer: the
+// w, w+16, ... and loads the samples of its next frame while it transforms
+// the current one.  Each wave owns a 256-entry complex f64 LDS buffer: the
 // 512-point real FFT is a 256-point complex FFT of z[n] = y[2n] + i y[2n+1]
 // (radix-4 Stockham, 4 in-place stages, one butterfly per lane; a wave's LDS
 // ops execute in order, so a stage's reads of all lanes precede its writes
@@ -41,10 +42,30 @@ constexpr int kWaves = 16, kThreads = kWaves * 64;
 
 // table layout (doubles): window[400] | cos256 | sin256 | cos512 | sin512 |
 //   start[80] | len[80] | off[80] | w[<=1024]
+// w is stored lane-interleaved and zero-padded to a fixed length per lane
+// group: bins 0..63 as w0[i][64] (i < kMelLen0), bins 64..79 as w1[i][16]
+// (i < kMelLen1).  Every lane of a group then runs the same unrolled loop,
+// the weight reads are lane-contiguous (no bank conflicts), and the padded
+// terms add w = 0 exactly (e + 0*p == e for the finite, non-negative sums),
+// so the sums equal the sparse form's bit for bit.
 constexpr int kTabWin = 0, kTabC256 = 400, kTabS256 = 656, kTabC512 = 912, kTabS512 = 1168,
               kTabStart = 1424, kTabLen = 1504, kTabOff = 1584, kTabW = 1664;
-constexpr int kTabSize = kTabW + 1024;
+// tw: per-lane twiddles of FFT stages 1..3 as (cos, sin) pairs, [stage][r-1][lane]:
+// lane-contiguous 16-B reads (the c256/s256 gathers at stride 4..12 doubles
+// conflicted 2-4 ways); same values as c256[m]/s256[m]
+constexpr int kTabTw = kTabW + 1024;
+constexpr int kTabSize = kTabTw + 3 * 3 * 64 * 2;
+constexpr int kMelLen0 = 10, kMelLen1 = 16;
+constexpr int kTabW1 = kTabW + kMelLen0 * 64;
+static_assert(kTabW1 + kMelLen1 * 16 <= kTabSize, "fbank interleaved mel table");
 static_assert(kTabSize == kFbankTableDoubles, "fbank table size");
+
+// Bank swizzle of a wave's 256-entry complex buffer: XOR of the low 4 index
+// bits by 5 * ((i >> 4) & 3).  Contiguous 16-lane accesses stay a permutation
+// of one 256-B row; the radix-4 Stockham writes of the first two stages
+// (stride 4 and stride-16 groups of 4) land on 16 distinct 16-B slots instead
+// of 4 (4-way bank conflicts otherwise).
+__device__ __forceinline__ int zsw(int i) { return i ^ (((i >> 4) & 3) * 5); }
 
 __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
@@ -57,6 +78,22 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
+}
+
+// lane l receives v of lane l-1 (DPP wave_shr:1); lane 0 receives `first`
+__device__ __forceinline__ double wave_shr1(double v, double first) {
+  const unsigned long long u = __double_as_longlong(v), f = __double_as_longlong(first);
+  const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)f, (int)(unsigned)u, 0x138, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(unsigned)(f >> 32), (int)(unsigned)(u >> 32), 0x138, 0xF,
+                                             0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+__device__ __forceinline__ double readlane63(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)u, 63);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(u >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 template <int kDtype>
@@ -92,8 +129,7 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
   __syncthreads();
 
   const double* win = s_tab + kTabWin;
-  const double* c256 = s_tab + kTabC256;
-  const double* s256 = s_tab + kTabS256;
+  const double2* tw = reinterpret_cast<const double2*>(s_tab + kTabTw);
   const double* c512 = s_tab + kTabC512;
   const double* s512 = s_tab + kTabS512;
   double2* buf = s_buf[wave];
@@ -103,27 +139,44 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
   // mel bins of this lane: bin0 = lane, bin1 = lane + 64 (< 80)
   const int bin1 = lane + 64;
   const bool has1 = bin1 < kNB;
-  const int st0 = (int)s_tab[kTabStart + lane], n0 = (int)s_tab[kTabLen + lane], o0 = (int)s_tab[kTabOff + lane];
-  const int st1 = has1 ? (int)s_tab[kTabStart + bin1] : 0, n1 = has1 ? (int)s_tab[kTabLen + bin1] : 0,
-            o1 = has1 ? (int)s_tab[kTabOff + bin1] : 0;
+  const int st0 = (int)s_tab[kTabStart + lane];
+  const int st1 = has1 ? (int)s_tab[kTabStart + bin1] : 0;
   double csum0 = 0.0, csum1 = 0.0;
 
-  for (int t = wave; t < T; t += kWaves) {
+  // raw samples of the wave's next frame, loaded one frame ahead so their
+  // latency hides behind the current frame's FFT (PCM16 and f32 values are
+  // exact in f32)
+  float ne[4], no[4];
+  auto fetch = [&](int t) {
     const long x0 = wbase + (long)t * kFS;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = lane + 64 * q;
+      ne[q] = no[q] = 0.f;
+      if (n < kFL / 2) {
+        ne[q] = (float)load_sample<kDtype>(wav, x0 + 2 * n);
+        no[q] = (float)load_sample<kDtype>(wav, x0 + 2 * n + 1);
+      }
+    }
+  };
+  if (wave < T) fetch(wave);
+
+  for (int t = wave; t < T; t += kWaves) {
     // 1. samples of z[n] = y[2n] + i y[2n+1], n = lane + 64q (n < 200 carries data)
     double xe[4], xo[4], xp[4];
     double sum = 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int n = lane + 64 * q;
-      xe[q] = xo[q] = xp[q] = 0.0;
-      if (n < kFL / 2) {
-        xe[q] = load_sample<kDtype>(wav, x0 + 2 * n) * dscale;
-        xo[q] = load_sample<kDtype>(wav, x0 + 2 * n + 1) * dscale;
-        xp[q] = n > 0 ? load_sample<kDtype>(wav, x0 + 2 * n - 1) * dscale : xe[q];  // replicate pad
-        sum += xe[q] + xo[q];
-      }
+      xe[q] = (double)ne[q] * dscale;
+      xo[q] = (double)no[q] * dscale;
+      if (n < kFL / 2) sum += xe[q] + xo[q];
     }
+    if (t + kWaves < T) fetch(t + kWaves);
+    // y[2n-1] is the odd sample of element n-1: lane-1's xo (wave_shr:1), or
+    // lane 63's xo of the previous q; n = 0 replicates y[0] (pre-emphasis pad)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xp[q] = wave_shr1(xo[q], q > 0 ? readlane63(xo[q - 1]) : xe[0]);
     // 2. DC removal, pre-emphasis, window (f64; exact sums for PCM16 input)
     const double mean = wave_sum_f64(sum) * (1.0 / kFL);
 #pragma unroll
@@ -135,7 +188,7 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
         z.x = (de - 0.97 * dp) * win[2 * n];
         z.y = (dd - 0.97 * de) * win[2 * n + 1];
       }
-      buf[n] = z;
+      buf[zsw(n)] = z;
     }
     wave_lds_fence();
     // 3. 256-point complex FFT, radix-4 Stockham, in place
@@ -145,12 +198,13 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
       const int k = j & (ns - 1);
       double2 a[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a[r] = buf[j + 64 * r];
+      for (int r = 0; r < 4; ++r) a[r] = buf[zsw(j + 64 * r)];
       if (ns > 1) {
+        const int stage = ns == 4 ? 0 : ns == 16 ? 1 : 2;
 #pragma unroll
         for (int r = 1; r < 4; ++r) {
-          const int m = r * k * (64 / ns);
-          const double c = c256[m], s = s256[m];
+          const double2 cs = tw[(stage * 3 + r - 1) * 64 + j];
+          const double c = cs.x, s = cs.y;
           // a *= exp(-i 2 pi m / 256) = c - i s
           const double re = a[r].x * c + a[r].y * s;
           const double im = a[r].y * c - a[r].x * s;
@@ -164,10 +218,10 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
       wave_lds_fence();
       // -i * d13 = (d13.y, -d13.x)
       const int d = (j / ns) * ns * 4 + k;
-      buf[d] = make_double2(s02.x + s13.x, s02.y + s13.y);
-      buf[d + ns] = make_double2(d02.x + d13.y, d02.y - d13.x);
-      buf[d + 2 * ns] = make_double2(s02.x - s13.x, s02.y - s13.y);
-      buf[d + 3 * ns] = make_double2(d02.x - d13.y, d02.y + d13.x);
+      buf[zsw(d)] = make_double2(s02.x + s13.x, s02.y + s13.y);
+      buf[zsw(d + ns)] = make_double2(d02.x + d13.y, d02.y - d13.x);
+      buf[zsw(d + 2 * ns)] = make_double2(s02.x - s13.x, s02.y - s13.y);
+      buf[zsw(d + 3 * ns)] = make_double2(d02.x - d13.y, d02.y + d13.x);
       wave_lds_fence();
     }
     // 4. even/odd split -> X[k], power |X[k]|^2 for k = 0..255 (Nyquist weight is 0)
@@ -177,8 +231,8 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int k = lane + 64 * q;
-        z[q] = buf[k];
-        zc[q] = buf[(256 - k) & 255];
+        z[q] = buf[zsw(k)];
+        zc[q] = buf[zsw((256 - k) & 255)];
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -201,14 +255,16 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
     float* frow = feats + (fbase + t) * kNB;
     {
       double e = 0.0;
-      for (int i = 0; i < n0; ++i) e += s_tab[kTabW + o0 + i] * pw[st0 + i];
+#pragma unroll
+      for (int i = 0; i < kMelLen0; ++i) e += s_tab[kTabW + i * 64 + lane] * pw[st0 + i];
       const float v = (float)log(fmax(e, (double)FLT_EPSILON));
       frow[lane] = v;
       csum0 += (double)v;
     }
     if (has1) {
       double e = 0.0;
-      for (int i = 0; i < n1; ++i) e += s_tab[kTabW + o1 + i] * pw[st1 + i];
+#pragma unroll
+      for (int i = 0; i < kMelLen1; ++i) e += s_tab[kTabW1 + i * 16 + (lane & 15)] * pw[st1 + i];
       const float v = (float)log(fmax(e, (double)FLT_EPSILON));
       frow[bin1] = v;
       csum1 += (double)v;
@@ -245,16 +301,24 @@ void fbank_tables(double* tab) {
     tab[kTabC512 + m] = std::cos(2.0 * kPi * m / 512.0);
     tab[kTabS512 + m] = std::sin(2.0 * kPi * m / 512.0);
   }
-  // mel filters: torchaudio get_mel_banks in float32 (generated table)
+  for (int st = 0, ns = 4; st < 3; ++st, ns *= 4)
+    for (int r = 1; r < 4; ++r)
+      for (int j = 0; j < 64; ++j) {
+        const int m = r * (j & (ns - 1)) * (64 / ns);
+        tab[kTabTw + ((st * 3 + r - 1) * 64 + j) * 2] = tab[kTabC256 + m];
+        tab[kTabTw + ((st * 3 + r - 1) * 64 + j) * 2 + 1] = tab[kTabS256 + m];
+      }
+  // mel filters: torchaudio get_mel_banks in float32 (generated table),
+  // stored lane-interleaved and zero-padded (see kMelLen0 / kMelLen1)
   int o = 0;
   for (int b = 0; b < kNB; ++b) {
+    const int len = b < 64 ? kMelLen0 : kMelLen1;
+    WSP_CHECK(kMelLen[b] <= len && kMelStart[b] + len <= 256, "fbank: mel table overflow");
     tab[kTabStart + b] = kMelStart[b];
     tab[kTabLen + b] = kMelLen[b];
     tab[kTabOff + b] = o;
-    for (int i = 0; i < kMelLen[b]; ++i, ++o) {
-      WSP_CHECK(o < 1024 && kMelStart[b] + i < 256, "fbank: mel table overflow");
-      tab[kTabW + o] = (double)kMelW[o];
-    }
+    for (int i = 0; i < kMelLen[b]; ++i, ++o)
+      tab[b < 64 ? kTabW + i * 64 + b : kTabW1 + i * 16 + (b - 64)] = (double)kMelW[o];
   }
   WSP_CHECK(o == kMelWeights, "fbank: mel table size");
 }

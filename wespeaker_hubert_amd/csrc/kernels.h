@@ -165,7 +165,7 @@ void launch_resnet_stem(const float* feats, int B, int T, int F, int C0, const f
 
 // Kaldi fbank (float64 arithmetic) + optional fused CMN.  `tables` = device
 // copy of fbank_tables().
-constexpr int kFbankTableDoubles = 1664 + 1024;
+constexpr int kFbankTableDoubles = 1664 + 1024 + 1152;
 void fbank_tables(double* host_tab);  // window, twiddles, sparse mel filters
 // Segmented: wseg / fseg = device int32 [B+1] sample / frame offsets, T = frames
 // of the longest utterance (grid size); N, ld unused.
