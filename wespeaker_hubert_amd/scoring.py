@@ -155,11 +155,8 @@ def trials_cosine_score(emb: Dict[str, np.ndarray], trials: Sequence[str], store
         sc = cosine_pairs(E, ia, ib)
         path = os.path.join(store_dir, os.path.basename(trial) + ".score")
         with open(path, "w") as w:
-            for s, v in zip(lines, sc):
-                if len(s) == 3:
-                    w.write("{} {} {:.5f} {}\n".format(s[0], s[1], v, s[2]))
-                else:
-                    w.write("{} {} {:.5f}\n".format(s[0], s[1], v))
+            w.write("".join(f"{s[0]} {s[1]} {v:.5f} {s[2]}\n" if len(s) == 3 else f"{s[0]} {s[1]} {v:.5f}\n"
+                            for s, v in zip(lines, np.asarray(sc, np.float64).tolist())))
         out_paths.append(path)
     return out_paths
 
@@ -188,13 +185,18 @@ def score_norm(score_norm_method: str, top_n: int, trial_score_file: str, score_
     ti = {k: i for i, k in enumerate(test)}
     e_mag = np.linalg.norm(Ee - mv, axis=1)
     t_mag = np.linalg.norm(Et - mv, axis=1)
+    # whole-trial-list arithmetic in the per-row order of score_norm.py:103-111 (float64, so
+    # every value and every formatted line equals the per-row form), one write
+    n = len(rows)
+    ia = np.fromiter((ei[r[0]] for r in rows), np.int64, n)
+    ib = np.fromiter((ti[r[1]] for r in rows), np.int64, n)
+    s = np.fromiter((float(r[2]) for r in rows), np.float64, n)
+    ns = 0.5 * ((s - e_mu[ia]) / e_sd[ia] + (s - t_mu[ib]) / t_sd[ib])
     with open(score_norm_file, "w", encoding="utf-8") as fout:
-        for r in rows:
-            a, b = ei[r[0]], ti[r[1]]
-            s = float(r[2])
-            ns = 0.5 * ((s - e_mu[a]) / e_sd[a] + (s - t_mu[b]) / t_sd[b])
-            fout.write("{} {} {:.5f} {} {:.4f} {:.4f} {:.4f} {:.4f}\n".format(
-                r[0], r[1], ns, r[3], e_mag[a], t_mag[b], e_mu[a], t_mu[b]))
+        fout.write("".join(
+            f"{r[0]} {r[1]} {v:.5f} {r[3]} {ma:.4f} {mb:.4f} {ua:.4f} {ub:.4f}\n"
+            for r, v, ma, mb, ua, ub in zip(rows, ns.tolist(), e_mag[ia].tolist(), t_mag[ib].tolist(),
+                                            e_mu[ia].tolist(), t_mu[ib].tolist())))
 
 
 def compute_metrics(scores_file: str, p_target=0.01, c_miss=1, c_fa=1) -> Tuple[float, float]:
