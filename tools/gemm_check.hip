@@ -4,7 +4,8 @@
 // 1x1 with Ti != T).  Family 7 must equal family 6 bit for bit (outputs and SE column sums); then
 // interleaved timing rounds.  (r5's family 8, a ping-pong k-loop, and family 9, family 7 on 16 waves
 // of 64 x 64 or 8 waves of 32 x 256, and a persistent family 7, were measured with this tool and
-// pruned: profiles/r5a_gemm_check.txt, r5m_gemm_family9.txt, r5p_gemm_persistent.txt.)
+// pruned: profiles/r5a_gemm_check.txt, r5m_gemm_family9.txt, r5p_gemm_persistent.txt; a staggered
+// start of every other CU's first block, r5ac_gemm_stagger_experiment.txt.)
 //   gemm_check [case|all] [reps] [variants, e.g. 67]
 #include <hip/hip_runtime.h>
 #include <cstdio>
