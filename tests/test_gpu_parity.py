@@ -115,6 +115,27 @@ def test_resnet_matches_oracle(arch, B, T):
     _assert_emb(emb.cpu().numpy(), ref.numpy())
 
 
+@pytest.mark.parametrize("feat_dim", [136, 72])
+def test_resnet_split_k_head_partial_slice(feat_dim):
+    """The TSTP head's split-K linear (ops.hip small_linear_splitk_kernel, K >= 4096): feat_dim 136
+    gives K = 2 * 256 * 17 = 8704, 28 slices of 320 with a partial last one; 72 gives K = 4608,
+    18 slices of 256.  Against the oracle, and every row equal to its batch-of-one result (the
+    slicing depends on K alone)."""
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    m = HipSpeakerModel("ResNet18", feat_dim=feat_dim, embed_dim=256)
+    sd = synth_state_dict(19, m.state_dict_layout(), residual_tame=True)
+    m.load_state_dict(sd)
+    m.to(DEV)
+    x = synth_feats(96, 3, 40, feat_dim)
+    _, emb = m(torch.from_numpy(x).to(DEV))
+    with torch.no_grad():
+        _, ref = models_ref.forward("ResNet18", torch.from_numpy(x), {k: torch.from_numpy(v) for k, v in sd.items()})
+    _assert_emb(emb.cpu().numpy(), ref.numpy())
+    for i in range(3):
+        _, one = m(torch.from_numpy(x[i:i + 1]).to(DEV))
+        np.testing.assert_array_equal(one.cpu().numpy()[0], emb.cpu().numpy()[i])
+
+
 @pytest.mark.parametrize("path", SIMAM_FIX, ids=[os.path.basename(p)[:-4] for p in SIMAM_FIX])
 def test_simam_matches_reference_fixture(path):
     """SimAM_ResNet{34,100}_ASP (samresnet.py) vs the reference module's own outputs."""
