@@ -62,17 +62,41 @@ constexpr int kTabW1 = kTabW + kMelLen0 * 64;
 static_assert(kTabW1 + kMelLen1 * 16 <= kTabSize, "fbank interleaved mel table");
 static_assert(kTabSize == kFbankTableDoubles, "fbank table size");
 
-// Bank swizzle of a wave's 256-entry complex buffer: XOR of the low 4 index
-// bits by 5 * ((i >> 4) & 3).  Contiguous 16-lane accesses stay a permutation
-// of one 256-B row; the radix-4 Stockham writes of the first two stages
-// (stride 4 and stride-16 groups of 4) land on 16 distinct 16-B slots instead
-// of 4 (4-way bank conflicts otherwise).
-__device__ __forceinline__ int zsw(int i) { return i ^ (((i >> 4) & 3) * 5); }
+// Bank swizzle of a wave's 256-entry complex buffer (16-B entries, 16 slots per
+// 256-B row): odd rows XOR the low 4 index bits by 13.  ds_write_b128 serves
+// 8 contiguous lanes per cycle: the radix-4 Stockham writes of the first two
+// stages (index 4j + m, and 16 (j >> 2) + (j & 3) + 4m) put those 8 lanes on an
+// even and an odd row with equal low bits, which the XOR (13 differs from 0 in
+// both bit pairs) separates.  ds_read_b128 serves the lane groups {0-3, 12-15,
+// 20-27}, {4-11, 16-19, 28-31} (+32): for a contiguous read, row 2r's entries
+// {0-3, 12-15} and row 2r+1's {4-11} stay disjoint under XOR 13 (it maps
+// {4-11} onto itself), so contiguous reads and writes stay conflict-free.
+__device__ __forceinline__ int zsw(int i) { return i ^ (((i >> 4) & 1) * 13); }
 
+// 64-bit DPP move (both halves with one control; lanes the masks leave out get 0)
+#define WSP_DPP64(v, ctrl, rmask)                                                                               \
+  __longlong_as_double(                                                                                         \
+      (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_update_dpp(                                   \
+                       0, (int)(unsigned)((unsigned long long)__double_as_longlong(v) >> 32), ctrl, rmask, 0xF, \
+                       false)                                                                                   \
+                   << 32) |                                                                                     \
+                  (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)__double_as_longlong(v), ctrl, rmask,  \
+                                                        0xF, false)))
+
+// Sum over the wave, uniform result: DPP pairs / quads / half-rows / rows, then
+// row_bcast15 / row_bcast31 into lane 63 (VALU latency instead of six
+// ds_bpermute round trips); fixed order, so deterministic and batch-independent.
 __device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += WSP_DPP64(v, 0xB1, 0xF);   // quad_perm [1,0,3,2]
+  v += WSP_DPP64(v, 0x4E, 0xF);   // quad_perm [2,3,0,1]
+  v += WSP_DPP64(v, 0x141, 0xF);  // row_half_mirror
+  v += WSP_DPP64(v, 0x140, 0xF);  // row_mirror: every lane holds its row's sum
+  v += WSP_DPP64(v, 0x142, 0xA);  // row_bcast15: rows 1, 3 += rows 0, 2
+  v += WSP_DPP64(v, 0x143, 0xC);  // row_bcast31: rows 2, 3 += lane 31 (rows 0 + 1)
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)u, 63);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(u >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 // Orders this wave's LDS accesses (a compiler scheduling fence; the hardware
