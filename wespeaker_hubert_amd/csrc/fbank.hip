@@ -205,6 +205,9 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
     for (int q = 0; q < 4; ++q) xp[q] = wave_shr1(xo[q], q > 0 ? readlane63(xo[q - 1]) : xe[0]);
     // 2. DC removal, pre-emphasis, window (f64; exact sums for PCM16 input)
     const double mean = wave_sum_f64(sum) * (1.0 / kFL);
+    // z[n] for n = lane + 64q stays in registers: it is exactly what the first
+    // Stockham stage's butterfly of this lane reads (a[r] = z[lane + 64 r])
+    double2 zin[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int n = lane + 64 * q;
@@ -214,17 +217,18 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
         z.x = (de - 0.97 * dp) * win[2 * n];
         z.y = (dd - 0.97 * de) * win[2 * n + 1];
       }
-      buf[zsw(n)] = z;
+      zin[q] = z;
     }
-    wave_lds_fence();
-    // 3. 256-point complex FFT, radix-4 Stockham, in place
+    // 3. 256-point complex FFT, radix-4 Stockham, in place; the last stage's
+    // outputs j + 64 m are also kept in registers (zl: the split's own-lane reads)
+    double2 zl[4];
 #pragma unroll
     for (int ns = 1; ns < 256; ns *= 4) {
       const int j = lane;
       const int k = j & (ns - 1);
       double2 a[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a[r] = buf[zsw(j + 64 * r)];
+      for (int r = 0; r < 4; ++r) a[r] = ns == 1 ? zin[r] : buf[zsw(j + 64 * r)];
       if (ns > 1) {
         const int stage = ns == 4 ? 0 : ns == 16 ? 1 : 2;
 #pragma unroll
@@ -244,10 +248,20 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
       wave_lds_fence();
       // -i * d13 = (d13.y, -d13.x)
       const int d = (j / ns) * ns * 4 + k;
-      buf[zsw(d)] = make_double2(s02.x + s13.x, s02.y + s13.y);
-      buf[zsw(d + ns)] = make_double2(d02.x + d13.y, d02.y - d13.x);
-      buf[zsw(d + 2 * ns)] = make_double2(s02.x - s13.x, s02.y - s13.y);
-      buf[zsw(d + 3 * ns)] = make_double2(d02.x - d13.y, d02.y + d13.x);
+      const double2 o0 = make_double2(s02.x + s13.x, s02.y + s13.y);
+      const double2 o1 = make_double2(d02.x + d13.y, d02.y - d13.x);
+      const double2 o2 = make_double2(s02.x - s13.x, s02.y - s13.y);
+      const double2 o3 = make_double2(d02.x - d13.y, d02.y + d13.x);
+      buf[zsw(d)] = o0;
+      buf[zsw(d + ns)] = o1;
+      buf[zsw(d + 2 * ns)] = o2;
+      buf[zsw(d + 3 * ns)] = o3;
+      if (ns == 64) {  // d = j: outputs j, j + 64, j + 128, j + 192
+        zl[0] = o0;
+        zl[1] = o1;
+        zl[2] = o2;
+        zl[3] = o3;
+      }
       wave_lds_fence();
     }
     // 4. even/odd split -> X[k], power |X[k]|^2 for k = 0..255 (Nyquist weight is 0)
@@ -257,7 +271,7 @@ __global__ __launch_bounds__(kThreads) void fbank_cmn_kernel(const void* __restr
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int k = lane + 64 * q;
-        z[q] = buf[zsw(k)];
+        z[q] = zl[q];
         zc[q] = buf[zsw((256 - k) & 255)];
       }
 #pragma unroll
