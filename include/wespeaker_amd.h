@@ -54,8 +54,13 @@ extern "C" {
 #define WSP_DTYPE_F32 0
 #define WSP_DTYPE_S16 1
 
+/* kaldi.fbank window_type (torchaudio compliance/kaldi.py _feature_window_function;
+ * Speaker.set_window_type, cli/speaker.py:62) */
 #define WSP_WINDOW_HAMMING 0
 #define WSP_WINDOW_POVEY 1
+#define WSP_WINDOW_HANNING 2
+#define WSP_WINDOW_RECTANGULAR 3
+#define WSP_WINDOW_BLACKMAN 4
 
 typedef struct wsp_model wsp_model;
 
@@ -67,15 +72,42 @@ const char* wsp_last_error(void);
  * 0 when num_samples < frame_len. */
 int wsp_fbank_num_frames(int num_samples, int frame_len, int frame_shift);
 
-/* Batched Kaldi log-mel fbank (80 bins, 25 ms / 10 ms @16 kHz, 512-pt FFT,
- * dither 0, DC removal, pre-emphasis 0.97, hamming window).
+/* torchaudio.compliance.kaldi.fbank options on the extraction path
+ * (dataset_args.fbank_args -> processor.compute_fbank, processor.py:472-502;
+ * Speaker.compute_fbank, cli/speaker.py:89-104).  Fixed as the reference
+ * calls it: dither 0 (bin/extract.py:66-67), DC removal, pre-emphasis 0.97,
+ * snip edges, power spectrum, log, no energy, no VTLN.  Implemented: 4..128
+ * bins and any frame that pads to 256 or 512 samples (25 ms at 8 or 16 kHz,
+ * examples/sre/v2,v3/conf/resnet.yaml and the voxceleb recipes). */
+typedef struct wsp_fbank_opts {
+  int num_mel_bins;       /* 80 */
+  int sample_rate;        /* sample_frequency, Hz (16000) */
+  double frame_length_ms; /* 25 */
+  double frame_shift_ms;  /* 10 */
+  int window_type;        /* WSP_WINDOW_* (hamming) */
+  double low_freq;        /* 20 */
+  double high_freq;       /* 0 = Nyquist; < 0 = offset below Nyquist */
+} wsp_fbank_opts;
+
+/* Fills torchaudio's defaults with the reference's window (hamming). */
+int wsp_fbank_opts_default(wsp_fbank_opts* o);
+/* Frame geometry of `o`: samples per frame / shift (int(sr * ms * 0.001)) and
+ * the padded FFT size; WSP_E_INVALID for options outside the set above. */
+int wsp_fbank_geometry(const wsp_fbank_opts* o, int* frame_len, int* frame_shift, int* padded);
+/* Host-only: torchaudio get_mel_banks(num_mel_bins, padded, ...) as the kernel
+ * uses it, banks = [num_mel_bins][padded / 2 + 1] f32 (Nyquist column 0). */
+int wsp_fbank_mel_banks(const wsp_fbank_opts* o, float* banks);
+
+/* Batched Kaldi log-mel fbank.
  *   wav    [B][ld] samples (f32 or s16), first num_samples of each row used
  *   scale  multiplies samples first (32768 for [-1,1] input on the
  *          dataset path, processor.py:492; 1 for int16-valued input)
- *   feats  [B][T][num_bins] f32, T = wsp_fbank_num_frames(num_samples,...)
- *   cmn    1: subtract the per-utterance mean over frames (speaker.py:102-103)
- * Only num_bins = 80, sample_rate = 16000, frame 400 / shift 160 and the
- * hamming window are implemented (the north-star configuration). */
+ *   feats  [B][T][num_mel_bins] f32, T = wsp_fbank_num_frames(num_samples,
+ *          frame_len, frame_shift) of wsp_fbank_geometry
+ *   cmn    1: subtract the per-utterance mean over frames (speaker.py:102-103) */
+int wsp_fbank_ex(const void* wav, int wav_dtype, int B, int num_samples, int ld, float scale,
+                 float* feats, const wsp_fbank_opts* opts, int cmn, void* stream);
+/* Same with 25 ms / 10 ms frames and 20 Hz .. Nyquist filters. */
 int wsp_fbank(const void* wav, int wav_dtype, int B, int num_samples, int ld, float scale,
               float* feats, int num_bins, int sample_rate, int window_type, int cmn,
               void* stream);
@@ -86,7 +118,11 @@ int wsp_fbank(const void* wav, int wav_dtype, int B, int num_samples, int ld, fl
  * without per-utterance launches.  Device int32 offsets: utterance b = samples
  * [sample_offsets[b], sample_offsets[b+1]) of `wav` and frames
  * [frame_offsets[b], frame_offsets[b+1]) of `feats` (frames_b =
- * wsp_fbank_num_frames(samples_b, 400, 160) >= 1); max_frames = largest frames_b. */
+ * wsp_fbank_num_frames(samples_b, frame_len, frame_shift) >= 1); max_frames =
+ * largest frames_b. */
+int wsp_fbank_segments_ex(const void* wav, int wav_dtype, int B, const int32_t* sample_offsets,
+                          const int32_t* frame_offsets, int max_frames, float scale, float* feats,
+                          const wsp_fbank_opts* opts, int cmn, void* stream);
 int wsp_fbank_segments(const void* wav, int wav_dtype, int B, const int32_t* sample_offsets,
                        const int32_t* frame_offsets, int max_frames, float scale, float* feats,
                        int num_bins, int sample_rate, int window_type, int cmn, void* stream);
@@ -226,6 +262,13 @@ int wsp_frontend_forward_segments(wsp_model* m, const float* wav, int B, const i
  * (wespeaker/cli/speaker.py:106-110, np.mean over axis 1) and apply_cmvn(norm_mean)
  * (wespeaker/dataset/dataset_utils.py:19-26) on feature tensors already on the device. */
 int wsp_cmn(float* x, int B, int T, int D, void* stream);
+/* apply_cmvn(feats, norm_mean, norm_var) of wespeaker/dataset/dataset_utils.py:19-26
+ * as bin/extract.py:104-106 applies it with dataset_args.cmvn_args: per utterance,
+ * x -= mean over frames (norm_mean), then x /= sqrt(var over frames (unbiased) +
+ * 1e-7) (norm_var; T = 1 gives NaN, as torch.var).  x [B][T][D] in place, or a
+ * ragged batch: frame_offsets = device int32 [B+1] row offsets (T ignored). */
+int wsp_cmvn(float* x, int B, int T, int D, const int32_t* frame_offsets, int norm_mean, int norm_var,
+             void* stream);
 
 /* --------------------------------------------------------- resampling --- */
 /* Replaces torchaudio.transforms.Resample(orig_freq, new_freq) as the reference

@@ -5,8 +5,11 @@ reference, `requirements.txt` torchaudio>=0.12, unpinned; NOT installed here)
 exactly as the reference calls it:
 
   * cli/speaker.py:89-104  kaldi.fbank(num_mel_bins=80, frame_length=25,
-    frame_shift=10, sample_frequency=sr, window_type=hamming) then CMN
+    frame_shift=10, sample_frequency=sr, window_type=self.window_type) then CMN
     `feat - mean(feat, 0)`; dither / energy at torchaudio defaults (0.0/False).
+    Windows: kaldi.py _feature_window_function (hamming, hanning, povey,
+    rectangular, blackman).  Recipes' fbank_args: num_mel_bins 40 / 64 / 72 / 80
+    at 8 or 16 kHz (examples/sre/v2,v3/conf/resnet.yaml: 40 / 64 bins).
   * dataset/processor.py:472-502  same with `wav * (1 << 15)` and dither
     forced to 0.0 by bin/extract.py:66-67.
 
@@ -84,28 +87,42 @@ def _frames(wave: np.ndarray, frame_len: int, frame_shift: int) -> np.ndarray:
     return wave[idx]
 
 
-def _window(frame_len, dtype):
+def _window(frame_len, dtype, window_type="hamming"):
+    """kaldi.py _feature_window_function (symmetric windows; blackman_coeff 0.42)."""
     n = np.arange(frame_len, dtype=np.float64)
-    return (0.54 - 0.46 * np.cos(2 * np.pi * n / (frame_len - 1))).astype(dtype)
+    a = 2 * np.pi * n / (frame_len - 1)
+    if window_type == "hamming":
+        w = 0.54 - 0.46 * np.cos(a)
+    elif window_type == "hanning":
+        w = 0.5 - 0.5 * np.cos(a)
+    elif window_type == "povey":
+        w = (0.5 - 0.5 * np.cos(a)) ** 0.85
+    elif window_type == "rectangular":
+        w = np.ones(frame_len)
+    elif window_type == "blackman":
+        w = 0.42 - 0.5 * np.cos(a) + 0.08 * np.cos(2 * a)
+    else:
+        raise ValueError(f"Invalid window type {window_type}")
+    return w.astype(dtype)
 
 
-def _prep(wave, frame_len, frame_shift, dtype, preemph=0.97):
+def _prep(wave, frame_len, frame_shift, dtype, preemph=0.97, window_type="hamming"):
     x = _frames(np.asarray(wave, dtype=dtype), frame_len, frame_shift)
     x = x - x.mean(axis=1, keepdims=True)
     prev = np.concatenate([x[:, :1], x[:, :-1]], axis=1)
     x = x - dtype(preemph) * prev
-    return (x * _window(frame_len, dtype)[None, :]).astype(dtype)
+    return (x * _window(frame_len, dtype, window_type)[None, :]).astype(dtype)
 
 
 def fbank(wave, num_mel_bins=80, frame_length_ms=25.0, frame_shift_ms=10.0, sample_freq=16000.0,
-          dtype=np.float64, cmn=False) -> np.ndarray:
+          dtype=np.float64, cmn=False, window_type="hamming") -> np.ndarray:
     """(T, num_mel_bins) log-mel, computed in `dtype` with numpy's FFT."""
     fl = int(sample_freq * frame_length_ms * 0.001)
     fs = int(sample_freq * frame_shift_ms * 0.001)
     if len(wave) < fl:
         return np.zeros((0, num_mel_bins), dtype=np.float32)
     padded = 1 << int(np.ceil(np.log2(fl)))
-    x = _prep(wave, fl, fs, dtype)
+    x = _prep(wave, fl, fs, dtype, window_type=window_type)
     spec = np.fft.rfft(x, n=padded, axis=1)
     power = (spec.real ** 2 + spec.imag ** 2).astype(dtype)
     banks = mel_banks(num_mel_bins, padded, sample_freq).astype(dtype)
@@ -118,6 +135,18 @@ def fbank(wave, num_mel_bins=80, frame_length_ms=25.0, frame_shift_ms=10.0, samp
         # mean is taken in float64 here.
         out = (out - out.astype(np.float64).mean(axis=0, keepdims=True)).astype(np.float32)
     return out
+
+
+def apply_cmvn(feats, norm_mean=True, norm_var=False):
+    """dataset_utils.py:19-26 on (B, T, F) float32, statistics in float64."""
+    x = np.asarray(feats, dtype=np.float64)
+    if norm_mean:
+        x = x - x.mean(axis=1, keepdims=True)
+        x = x.astype(np.float32).astype(np.float64)
+    if norm_var:
+        with np.errstate(invalid="ignore", divide="ignore"):
+            x = x / np.sqrt(x.var(axis=1, ddof=1, keepdims=True) + 1e-7)
+    return x.astype(np.float32)
 
 
 def fbank_dft64(wave, num_mel_bins=80, sample_freq=16000.0) -> np.ndarray:

@@ -248,8 +248,12 @@ void HipSpeakerModel::ExtractEmbedding(const std::vector<std::vector<float>>& fe
 HipSpeakerEngine::HipSpeakerEngine(const std::string& model_path, int feat_dim, int sample_rate,
                                    int embedding_size, int samples_per_chunk, int device)
     : feat_dim_(feat_dim), sample_rate_(sample_rate), per_chunk_samples_(samples_per_chunk) {
-  if (sample_rate != 16000 || feat_dim != 80)
-    throw std::invalid_argument("HipSpeakerEngine: fbank is implemented for 80 bins at 16 kHz");
+  // FeaturePipelineConfig(num_bins, sample_rate): 25 / 10 ms frames (feature_pipeline.h:35-39)
+  wsp_fbank_opts o;
+  wsp_fbank_opts_default(&o);
+  o.num_mel_bins = feat_dim;
+  o.sample_rate = sample_rate;
+  Check(wsp_fbank_geometry(&o, &frame_len_, &frame_shift_, nullptr), "wsp_fbank_geometry");
   model_ = std::make_unique<HipSpeakerModel>(model_path, device);
   if (model_->FeatDim() != feat_dim) throw std::invalid_argument("HipSpeakerEngine: model feat_dim differs");
   embedding_size_ = model_->EmbedDim();
@@ -263,7 +267,7 @@ HipSpeakerEngine::HipSpeakerEngine(const std::string& model_path, int feat_dim, 
 void HipSpeakerEngine::ExtractFeature(const int16_t* data, int data_size,
                                       std::vector<std::vector<std::vector<float>>>* chunks_feat) {
   if (!data) throw std::invalid_argument("ExtractFeature: input is nullptr");
-  const int T = wsp_fbank_num_frames(data_size, 400, 160);
+  const int T = wsp_fbank_num_frames(data_size, frame_len_, frame_shift_);
   if (T <= 0) throw std::invalid_argument("ExtractFeature: fewer samples than one frame");
   hipStream_t s = static_cast<hipStream_t>(stream_);
   auto grow = [](void** p, size_t* cap, size_t need) {

@@ -95,6 +95,7 @@ class HipSpeakerEngine {
   void* stream_ = nullptr;
   void* d_wav_ = nullptr;
   float* d_fbank_ = nullptr;
+  int frame_len_ = 400, frame_shift_ = 160;  // samples (wsp_fbank_geometry)
   size_t cap_wav_ = 0, cap_fbank_ = 0;
 };
 

@@ -118,3 +118,37 @@ def test_option_defaults_and_streams_workspace():
                 assert b1.value // 2 < b2.value <= b1.value + 3 * 65536
         finally:
             lib.wsp_model_destroy(h)
+
+
+def test_fbank_host_tables_match_oracle():
+    """The kernel's mel filters are computed by the library's own host code
+    (fbank.hip fbank_mel_banks, torchaudio get_mel_banks' float32 arithmetic): bit-identical
+    to the oracle's independent numpy restatement for every recipe configuration."""
+    import numpy as np
+    from oracle.fbank_ref import mel_banks
+    from wespeaker_hubert_amd.frontend import FbankArgs
+    for nb in (23, 40, 64, 72, 80, 128):
+        for sr in (8000, 16000):
+            a = FbankArgs(nb, sample_rate=sr)
+            fl, fs, padded = a.geometry()
+            assert (fl, fs, padded) == ((200, 80, 256) if sr == 8000 else (400, 160, 512))
+            got = a.mel_banks()
+            ref = mel_banks(nb, padded, float(sr))
+            assert got.shape == ref.shape == (nb, padded // 2 + 1)
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (nb, sr)
+
+
+def test_fbank_geometry_rejects_unsupported():
+    import pytest
+    from wespeaker_hubert_amd.frontend import FbankArgs
+    assert FbankArgs(frame_length=32).geometry() == (512, 160, 512)
+    with pytest.raises(_lib.WspError, match="pad to 256 or 512"):
+        FbankArgs(frame_length=40).geometry()
+    with pytest.raises(_lib.WspError, match="num_mel_bins"):
+        FbankArgs(num_mel_bins=3).geometry()
+    with pytest.raises(_lib.WspError, match="too wide"):
+        FbankArgs(num_mel_bins=8).geometry()
+    with pytest.raises(ValueError, match="Invalid window type"):
+        FbankArgs(window_type="triangle").geometry()
+    for w in ("hamming", "hanning", "povey", "rectangular", "blackman"):
+        assert FbankArgs(window_type=w).geometry() == (400, 160, 512)

@@ -78,7 +78,7 @@ def _rank_main(rank, world, port, data_list, model_path, config, out_dir, q):
     torch.cuda.current_device = lambda: 0
     torch.cuda.device_count = lambda: 1
     ex.get_speaker_model = lambda name: _StubModel
-    ex.embed_utterances = lambda model, pcms, device, max_frames, frontend=None: [_stub_embedding(p) for p in pcms]
+    ex.embed_utterances = lambda model, pcms, device, max_frames, frontend=None, **kw: [_stub_embedding(p) for p in pcms]
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     scp = ex.extract(config=config, model_path=model_path, data_type="raw", data_list=data_list,

@@ -93,3 +93,33 @@ def test_subsegment_matches_reference_fixture():
         np.testing.assert_array_equal(np.stack(wins), z[f"wins_{n}"])
         n += 1
     assert n == 6
+
+
+def test_extraction_config_parsing():
+    """dataset_args -> fbank / cmvn options (bin/extract.py:66-67,104-106, processor.py:472-476)."""
+    import pytest
+    from wespeaker_hubert_amd.batching import Cmvn
+    from wespeaker_hubert_amd.frontend import FbankArgs
+    a = FbankArgs.from_config({"num_mel_bins": 64, "frame_shift": 10, "frame_length": 25, "dither": 1.0},
+                              sample_rate=8000)
+    assert a == FbankArgs(64, 25.0, 10.0, 8000, "hamming") and a.num_frames(8000) == 98
+    with pytest.raises(NotImplementedError):
+        FbankArgs.from_config({"use_energy": True})
+    assert Cmvn.from_config({}) == Cmvn(True, True, False)
+    c = Cmvn.from_config({"cmvn": True, "cmvn_args": {"norm_mean": True, "norm_var": True}})
+    assert c.mean and c.var
+    c = Cmvn.from_config({"cmvn": False, "cmvn_args": {"norm_var": True}})
+    assert not c.mean and not c.var
+    with pytest.raises(TypeError):
+        Cmvn.from_config({"cmvn_args": {"norm_std": True}})
+
+
+def test_oracle_apply_cmvn_matches_torch_formula():
+    """oracle.fbank_ref.apply_cmvn restates dataset_utils.py:19-26 (torch.var unbiased)."""
+    import torch
+    from oracle.fbank_ref import apply_cmvn
+    x = np.random.default_rng(1).standard_normal((2, 50, 8)).astype(np.float32) * 3 + 2
+    t = torch.from_numpy(x).double()
+    t = t - t.mean(dim=1, keepdim=True)
+    t = t / torch.sqrt(torch.var(t, dim=1, keepdim=True) + 1e-7)
+    np.testing.assert_allclose(apply_cmvn(x, True, True), t.numpy(), atol=2e-6)

@@ -34,3 +34,73 @@ def test_fire_parse():
     pos, kw = _fire.parse(["--exp_dir", "e", "--cal_mean", "True", "--batch-size", "16", "--top_n=300", "t1", "t2"])
     assert pos == ["t1", "t2"]
     assert kw == {"exp_dir": "e", "cal_mean": True, "batch_size": 16, "top_n": 300}
+
+
+# ----------------------------------------------------------- matrix reader --
+# Layouts from Kaldi's published sources (kaldi-matrix.cc Matrix::Read,
+# compressed-matrix.{h,cc}); the bytes below are written by hand, not by the reader.
+
+def _fm(rows, cols, data, tok=b"FM ", dt="<f4"):
+    return (b"\0B" + tok + b"\x04" + struct.pack("<i", rows) + b"\x04" + struct.pack("<i", cols)
+            + np.asarray(data, dtype=dt).tobytes())
+
+
+def test_load_mat_fm_dm_offsets_and_slices(tmp_path):
+    from wespeaker_hubert_amd.kaldi_io import load_mat
+    a = np.arange(12, dtype=np.float32).reshape(3, 4) * 0.5 - 1.0
+    b = np.arange(6, dtype=np.float64).reshape(2, 3) / 3.0
+    p = tmp_path / "m.ark"
+    blob = b"k1 " + _fm(3, 4, a) + b"k2 " + _fm(2, 3, b, b"DM ", "<f8")
+    p.write_bytes(blob)
+    off2 = len(b"k1 " + _fm(3, 4, a)) + 3
+    np.testing.assert_array_equal(load_mat(f"{p}:3"), a)
+    got = load_mat(f"{p}:{off2}")
+    assert got.dtype == np.float64
+    np.testing.assert_array_equal(got, b)
+    np.testing.assert_array_equal(load_mat(f"{p}:3[1:3]"), a[1:3])
+    np.testing.assert_array_equal(load_mat(f"{p}:3[0:2,1:3]"), a[0:2, 1:3])
+    np.testing.assert_array_equal(load_mat(str(p)), a)  # path alone: the first object after its key
+
+
+def test_load_mat_compressed_formats(tmp_path):
+    from wespeaker_hubert_amd.kaldi_io import load_mat
+    p = tmp_path / "c.ark"
+    # CM3 (kOneByte, row-major): min -1, range 255 -> increment (255 * (1/255.0)) = 1 exactly
+    q3 = np.array([[0, 1, 2], [250, 255, 7]], dtype=np.uint8)
+    cm3 = b"\0BCM3 " + struct.pack("<ffii", -1.0, 255.0, 2, 3) + q3.tobytes()
+    # CM2 (kTwoByte, row-major): min 2, range 65535 -> increment 1
+    q2 = np.array([[0, 65535], [12345, 7]], dtype="<u2")
+    cm2 = b"\0BCM2 " + struct.pack("<ffii", 2.0, 65535.0, 2, 2) + q2.tobytes()
+    # CM (kOneByteWithColHeaders): per-column u16 percentiles, bytes column-major;
+    # min 0, range 65535: Uint16ToFloat(v) = 65535 * 1.52590218966964e-05f * v
+    pct = np.array([[0, 100, 300, 1000], [10, 20, 30, 40]], dtype="<u2")
+    byt = np.array([[0, 64, 128, 192, 255], [32, 96, 160, 224, 200]], dtype=np.uint8)  # [col][row]
+    cm = b"\0BCM " + struct.pack("<ffii", 0.0, 65535.0, 5, 2) + pct.tobytes() + byt.tobytes()
+    blob = b"a " + cm3 + b"b " + cm2 + b"c " + cm
+    p.write_bytes(blob)
+    o_b = 2 + len(cm3) + 2
+    o_c = o_b + len(cm2) + 2
+    np.testing.assert_array_equal(load_mat(f"{p}:2"), q3.astype(np.float32) - 1.0)
+    np.testing.assert_array_equal(load_mat(f"{p}:{o_b}"), q2.astype(np.float32) + 2.0)
+    got = load_mat(f"{p}:{o_c}")
+    assert got.shape == (5, 2) and got.dtype == np.float32
+
+    def char_to_float(p0, p25, p75, p100, v):  # compressed-matrix.cc CharToFloat (in doubles)
+        if v <= 64:
+            return p0 + (p25 - p0) * v / 64.0
+        if v <= 192:
+            return p25 + (p75 - p25) * (v - 64) / 128.0
+        return p75 + (p100 - p75) * (v - 192) / 63.0
+    scale = 65535.0 * 1.52590218966964e-05
+    for c in range(2):
+        pc = [scale * float(x) for x in pct[c]]
+        for r in range(5):
+            want = char_to_float(*pc, int(byt[c, r]))
+            assert abs(got[r, c] - want) <= 1e-6 * max(1.0, abs(want)), (r, c, got[r, c], want)
+
+
+def test_load_mat_text(tmp_path):
+    from wespeaker_hubert_amd.kaldi_io import load_mat
+    p = tmp_path / "t.ark"
+    p.write_bytes(b"u1  [\n  1 2.5 -3\n  4 5 6 ]\n")
+    np.testing.assert_array_equal(load_mat(f"{p}:4"), np.array([[1, 2.5, -3], [4, 5, 6]], np.float32))

@@ -15,6 +15,20 @@ LIB_PATH = os.path.join(_HERE, "libwsp_hip.so")
 WSP_DTYPE_F32 = 0
 WSP_DTYPE_S16 = 1
 WSP_WINDOW_HAMMING = 0
+WSP_WINDOW_POVEY = 1
+WSP_WINDOW_HANNING = 2
+WSP_WINDOW_RECTANGULAR = 3
+WSP_WINDOW_BLACKMAN = 4
+# kaldi.fbank window_type names (torchaudio compliance/kaldi.py)
+WINDOW_TYPES = {"hamming": WSP_WINDOW_HAMMING, "povey": WSP_WINDOW_POVEY, "hanning": WSP_WINDOW_HANNING,
+                "rectangular": WSP_WINDOW_RECTANGULAR, "blackman": WSP_WINDOW_BLACKMAN}
+
+
+class FbankOpts(ctypes.Structure):
+    """wsp_fbank_opts (include/wespeaker_amd.h)."""
+    _fields_ = [("num_mel_bins", c_int), ("sample_rate", c_int), ("frame_length_ms", c_double),
+                ("frame_shift_ms", c_double), ("window_type", c_int), ("low_freq", c_double),
+                ("high_freq", c_double)]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -25,6 +39,12 @@ SIGNATURES = {
                           c_int, c_int, c_void_p]),
     "wsp_fbank_segments": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p, c_int,
                                    c_int, c_int, c_int, c_void_p]),
+    "wsp_fbank_opts_default": (c_int, [c_void_p]),
+    "wsp_fbank_geometry": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
+    "wsp_fbank_mel_banks": (c_int, [c_void_p, c_void_p]),
+    "wsp_fbank_ex": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_int, c_void_p]),
+    "wsp_fbank_segments_ex": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p,
+                                      c_void_p, c_int, c_void_p]),
     "wsp_model_create": (c_int, [c_char_p, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
     "wsp_model_destroy": (c_int, [c_void_p]),
     "wsp_model_num_params": (c_int, [c_void_p]),
@@ -53,6 +73,7 @@ SIGNATURES = {
     "wsp_model_profile_query": (c_int, [c_void_p, c_char_p, POINTER(c_int), POINTER(c_double),
                                         POINTER(c_double)]),
     "wsp_cmn": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "wsp_cmvn": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
     "wsp_resampler_create": (c_int, [c_int, c_int, c_int, c_float, c_void_p]),
     "wsp_resampler_destroy": (c_int, [c_void_p]),
     "wsp_resampler_out_len": (c_int, [c_void_p, c_int, c_void_p]),

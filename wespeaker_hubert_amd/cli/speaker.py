@@ -24,6 +24,7 @@ import yaml
 
 from ..audio import load_wav
 from ..batching import embed_utterances
+from ..frontend import FbankArgs
 from ..frontend import apply_cmn as _apply_cmn
 from ..frontend import compute_fbank as _gpu_fbank
 from ..kaldi_io import WriteHelper
@@ -54,8 +55,8 @@ class Speaker:
         self.wavform_norm = wavform_norm
 
     def set_window_type(self, window_type: str):
-        if window_type != 'hamming':
-            raise NotImplementedError("only the hamming window is implemented")
+        # kaldi.fbank window_type: hamming / hanning / povey / rectangular / blackman
+        # (an unknown name raises at the next fbank, as torchaudio does)
         self.window_type = window_type
 
     def set_resample_rate(self, resample_rate: int):
@@ -79,15 +80,15 @@ class Speaker:
     def compute_fbank(self, wavform, sample_rate=16000, num_mel_bins=80, frame_length=25,
                       frame_shift=10, cmn=True):
         """speaker.py:89-104 on the GPU; `wavform` (1, N) int16-valued."""
-        if (sample_rate, num_mel_bins, frame_length, frame_shift) != (16000, 80, 25, 10):
-            raise NotImplementedError("fbank implemented for 16 kHz, 80 bins, 25/10 ms")
+        args = FbankArgs(int(num_mel_bins), float(frame_length), float(frame_shift), int(sample_rate),
+                         self.window_type)
         if isinstance(wavform, torch.Tensor):
             x = wavform.to(device=self.device, dtype=torch.float32)
         else:
             x = torch.as_tensor(np.asarray(wavform), dtype=torch.float32).to(self.device)
         if x.dim() == 2:
             x = x[:1]
-        return _gpu_fbank(x, scale=1.0, cmn=cmn, window_type=self.window_type)[0]
+        return _gpu_fbank(x, scale=1.0, cmn=cmn, args=args)[0]
 
     # -------------------------------------------------------- embeddings --
     def extract_embedding_feats(self, fbanks, batch_size: int, subseg_cmn: bool) -> np.ndarray:
@@ -139,7 +140,9 @@ class Speaker:
                 names.append(name)
                 pcms.append(pcm)
         with torch.no_grad():
-            embeddings = embed_utterances(self.model, pcms, self.device)
+            embeddings = embed_utterances(self.model, pcms, self.device,
+                                          fbank_args=FbankArgs(sample_rate=self.resample_rate,
+                                                               window_type=self.window_type))
         return names, [np.asarray(e, dtype=np.float32) for e in embeddings]
 
     def compute_similarity(self, audio_path1: str, audio_path2: str) -> float:

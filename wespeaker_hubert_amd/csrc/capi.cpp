@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -17,23 +18,45 @@ static thread_local std::string g_err;
 void set_error(const std::string& m) { g_err = m; }
 const std::string& get_error() { return g_err; }
 
-// fbank tables, one device copy per device
-static const double* fbank_tables_dev() {
+// fbank plans (tables computed on the host at first use, one device copy per
+// device and configuration; never freed: a handful of KB per configuration)
+static const FbankPlan& fbank_plan_dev(const FbankConfig& c) {
   static std::mutex mu;
-  static std::vector<double*> per_dev;
+  static std::vector<std::unique_ptr<FbankPlan>> plans;
+  static std::vector<int> devs;
   int dev = 0;
   WSP_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(mu);
-  if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1, nullptr);
-  if (!per_dev[dev]) {
-    std::vector<double> h(kFbankTableDoubles);
-    fbank_tables(h.data());
-    double* d = nullptr;
-    WSP_HIP(hipMalloc(&d, h.size() * sizeof(double)));
-    WSP_HIP(hipMemcpy(d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-    per_dev[dev] = d;
+  for (size_t i = 0; i < plans.size(); ++i) {
+    const FbankConfig& q = plans[i]->cfg;
+    if (devs[i] == dev && q.num_bins == c.num_bins && q.sample_rate == c.sample_rate && q.window == c.window &&
+        q.frame_length_ms == c.frame_length_ms && q.frame_shift_ms == c.frame_shift_ms &&
+        q.low_freq == c.low_freq && q.high_freq == c.high_freq)
+      return *plans[i];
   }
-  return per_dev[dev];
+  auto p = std::make_unique<FbankPlan>();
+  fbank_plan(c, *p);
+  double* d = nullptr;
+  WSP_HIP(hipMalloc(&d, p->host_tab.size() * sizeof(double)));
+  WSP_HIP(hipMemcpy(d, p->host_tab.data(), p->host_tab.size() * sizeof(double), hipMemcpyHostToDevice));
+  p->tab = d;
+  plans.push_back(std::move(p));
+  devs.push_back(dev);
+  return *plans.back();
+}
+
+static FbankConfig fbank_config(const wsp_fbank_opts* o) {
+  WSP_CHECK(o != nullptr, "fbank: null options");
+  FbankConfig c;
+  c.num_bins = o->num_mel_bins;
+  c.sample_rate = o->sample_rate;
+  c.frame_length_ms = o->frame_length_ms;
+  c.frame_shift_ms = o->frame_shift_ms;
+  c.window = o->window_type;
+  c.low_freq = o->low_freq;
+  c.high_freq = o->high_freq;
+  fbank_config_resolve(c);
+  return c;
 }
 }  // namespace wsp
 
@@ -68,20 +91,74 @@ int wsp_fbank_num_frames(int num_samples, int frame_len, int frame_shift) {
   return 1 + (num_samples - frame_len) / frame_shift;
 }
 
+int wsp_fbank_opts_default(wsp_fbank_opts* o) {
+  if (!o) return WSP_E_INVALID;
+  o->num_mel_bins = 80;
+  o->sample_rate = 16000;
+  o->frame_length_ms = 25.0;
+  o->frame_shift_ms = 10.0;
+  o->window_type = WSP_WINDOW_HAMMING;
+  o->low_freq = 20.0;
+  o->high_freq = 0.0;
+  return WSP_OK;
+}
+
+int wsp_fbank_geometry(const wsp_fbank_opts* o, int* frame_len, int* frame_shift, int* padded) {
+  WSP_GUARD({
+    const wsp::FbankConfig c = wsp::fbank_config(o);
+    wsp::FbankPlan p;  // host tables only: rejects filters the kernel's LDS table cannot hold
+    wsp::fbank_plan(c, p);
+    if (frame_len) *frame_len = c.frame_len;
+    if (frame_shift) *frame_shift = c.frame_shift;
+    if (padded) *padded = c.padded;
+  });
+}
+
+int wsp_fbank_mel_banks(const wsp_fbank_opts* o, float* banks) {
+  WSP_GUARD({
+    WSP_CHECK(banks != nullptr, "fbank: null output");
+    std::vector<float> w;
+    wsp::fbank_mel_banks(wsp::fbank_config(o), w);
+    std::copy(w.begin(), w.end(), banks);
+  });
+}
+
+int wsp_fbank_ex(const void* wav, int wav_dtype, int B, int num_samples, int ld, float scale, float* feats,
+                 const wsp_fbank_opts* opts, int cmn, void* stream) {
+  WSP_GUARD({
+    const wsp::FbankConfig c = wsp::fbank_config(opts);
+    WSP_CHECK(wav_dtype == WSP_DTYPE_F32 || wav_dtype == WSP_DTYPE_S16, "fbank: bad dtype");
+    WSP_CHECK(B >= 0 && num_samples >= 0 && ld >= num_samples, "fbank: bad shape");
+    const int T = wsp_fbank_num_frames(num_samples, c.frame_len, c.frame_shift);
+    if (B > 0 && T > 0) {
+      WSP_CHECK(wav && feats, "fbank: null pointer");
+      wsp::launch_fbank(wav, wav_dtype, B, num_samples, ld, scale, feats, T, cmn, wsp::fbank_plan_dev(c), S(stream));
+    }
+  });
+}
+
 int wsp_fbank(const void* wav, int wav_dtype, int B, int num_samples, int ld, float scale,
               float* feats, int num_bins, int sample_rate, int window_type, int cmn,
               void* stream) {
+  wsp_fbank_opts o;
+  wsp_fbank_opts_default(&o);
+  o.num_mel_bins = num_bins;
+  o.sample_rate = sample_rate;
+  o.window_type = window_type;
+  return wsp_fbank_ex(wav, wav_dtype, B, num_samples, ld, scale, feats, &o, cmn, stream);
+}
+
+int wsp_fbank_segments_ex(const void* wav, int wav_dtype, int B, const int32_t* sample_offsets,
+                          const int32_t* frame_offsets, int max_frames, float scale, float* feats,
+                          const wsp_fbank_opts* opts, int cmn, void* stream) {
   WSP_GUARD({
-    WSP_CHECK(num_bins == 80, "fbank: only num_mel_bins=80 is implemented");
-    WSP_CHECK(sample_rate == 16000, "fbank: only 16 kHz is implemented");
-    WSP_CHECK(window_type == WSP_WINDOW_HAMMING, "fbank: only the hamming window is implemented");
+    const wsp::FbankConfig c = wsp::fbank_config(opts);
     WSP_CHECK(wav_dtype == WSP_DTYPE_F32 || wav_dtype == WSP_DTYPE_S16, "fbank: bad dtype");
-    WSP_CHECK(B >= 0 && num_samples >= 0 && ld >= num_samples, "fbank: bad shape");
-    const int T = wsp_fbank_num_frames(num_samples, 400, 160);
-    if (B > 0 && T > 0) {
-      WSP_CHECK(wav && feats, "fbank: null pointer");
-      wsp::launch_fbank(wav, wav_dtype, B, num_samples, ld, scale, feats, T, cmn,
-                        wsp::fbank_tables_dev(), S(stream));
+    WSP_CHECK(B >= 0 && max_frames >= 0, "fbank: bad shape");
+    if (B > 0 && max_frames > 0) {
+      WSP_CHECK(wav && feats && sample_offsets && frame_offsets, "fbank: null pointer");
+      wsp::launch_fbank(wav, wav_dtype, B, 0, 0, scale, feats, max_frames, cmn, wsp::fbank_plan_dev(c), S(stream),
+                        sample_offsets, frame_offsets);
     }
   });
 }
@@ -89,18 +166,13 @@ int wsp_fbank(const void* wav, int wav_dtype, int B, int num_samples, int ld, fl
 int wsp_fbank_segments(const void* wav, int wav_dtype, int B, const int32_t* sample_offsets,
                        const int32_t* frame_offsets, int max_frames, float scale, float* feats, int num_bins,
                        int sample_rate, int window_type, int cmn, void* stream) {
-  WSP_GUARD({
-    WSP_CHECK(num_bins == 80, "fbank: only num_mel_bins=80 is implemented");
-    WSP_CHECK(sample_rate == 16000, "fbank: only 16 kHz is implemented");
-    WSP_CHECK(window_type == WSP_WINDOW_HAMMING, "fbank: only the hamming window is implemented");
-    WSP_CHECK(wav_dtype == WSP_DTYPE_F32 || wav_dtype == WSP_DTYPE_S16, "fbank: bad dtype");
-    WSP_CHECK(B >= 0 && max_frames >= 0, "fbank: bad shape");
-    if (B > 0 && max_frames > 0) {
-      WSP_CHECK(wav && feats && sample_offsets && frame_offsets, "fbank: null pointer");
-      wsp::launch_fbank(wav, wav_dtype, B, 0, 0, scale, feats, max_frames, cmn, wsp::fbank_tables_dev(), S(stream),
-                        sample_offsets, frame_offsets);
-    }
-  });
+  wsp_fbank_opts o;
+  wsp_fbank_opts_default(&o);
+  o.num_mel_bins = num_bins;
+  o.sample_rate = sample_rate;
+  o.window_type = window_type;
+  return wsp_fbank_segments_ex(wav, wav_dtype, B, sample_offsets, frame_offsets, max_frames, scale, feats, &o, cmn,
+                               stream);
 }
 
 int wsp_model_create(const char* arch, int feat_dim, int embed_dim, int emb_bn, int two_emb_layer,
@@ -327,6 +399,15 @@ int wsp_cmn(float* x, int B, int T, int D, void* stream) {
   WSP_GUARD({
     WSP_CHECK(B >= 0 && T > 0 && D > 0 && (B == 0 || x), "bad argument");
     if (B > 0) wsp::launch_cmn_rows(x, B, T, D, S(stream));
+  });
+}
+
+int wsp_cmvn(float* x, int B, int T, int D, const int32_t* frame_offsets, int norm_mean, int norm_var,
+             void* stream) {
+  WSP_GUARD({
+    WSP_CHECK(B >= 0 && D > 0 && (frame_offsets || T > 0) && (B == 0 || x), "bad argument");
+    if (B > 0 && (norm_mean || norm_var))
+      wsp::launch_cmvn_rows(x, B, T, D, norm_mean != 0, norm_var != 0, S(stream), frame_offsets);
   });
 }
 

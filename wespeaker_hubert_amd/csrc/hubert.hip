@@ -230,24 +230,51 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LayerNormArgs p) {
 
 // ------------------------------------------------------------- cmn_rows ---
 // Block = (64 channels, utterance); 4 row groups of 64 lanes: coalesced
-// 256-B row segments, partial sums combined through LDS.
+// 256-B row segments, partial sums combined through LDS.  mode bit 0: mean
+// removal; bit 1: division by sqrt(unbiased variance + 1e-7) (apply_cmvn's
+// norm_var, dataset_utils.py:24-25), the variance taken about the mean of the
+// values as they are after bit 0 (torch.var centres itself).
+__device__ __forceinline__ double cmn_block_sum(double s, double (*part)[64]) {
+  part[threadIdx.x >> 6][threadIdx.x & 63] = s;
+  __syncthreads();
+  const int l = threadIdx.x & 63;
+  const double r = part[0][l] + part[1][l] + part[2][l] + part[3][l];
+  __syncthreads();  // part is reused by the next reduction
+  return r;
+}
+
 __global__ __launch_bounds__(256) void cmn_rows_kernel(float* __restrict__ x, int T_, int D,
-                                                       const int* __restrict__ seg) {
+                                                       const int* __restrict__ seg, int mode) {
   // f64 partial sums in a fixed order (torch's float32 mean is cascade-summed,
   // i.e. ~exact; a plain f32 running sum drifts ~1e-5 at a few hundred frames)
   __shared__ double part[4][64];
   const int b = blockIdx.y, c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
   const int T = seg ? seg[b + 1] - seg[b] : T_;
   float* p = x + (seg ? (size_t)seg[b] : (size_t)b * T_) * D + c;
-  double s = 0.0;
-  if (c < D)
-    for (int t = g; t < T; t += 4) s += (double)p[(size_t)t * D];
-  part[g][threadIdx.x & 63] = s;
-  __syncthreads();
-  const double mean = (part[0][threadIdx.x & 63] + part[1][threadIdx.x & 63] + part[2][threadIdx.x & 63] +
-                       part[3][threadIdx.x & 63]) / (double)T;
-  if (c < D)
-    for (int t = g; t < T; t += 4) p[(size_t)t * D] = (float)((double)p[(size_t)t * D] - mean);
+  if (mode & 1) {
+    double s = 0.0;
+    if (c < D)
+      for (int t = g; t < T; t += 4) s += (double)p[(size_t)t * D];
+    const double mean = cmn_block_sum(s, part) / (double)T;
+    if (c < D)
+      for (int t = g; t < T; t += 4) p[(size_t)t * D] = (float)((double)p[(size_t)t * D] - mean);
+  }
+  if (mode & 2) {
+    double s = 0.0;
+    if (c < D)
+      for (int t = g; t < T; t += 4) s += (double)p[(size_t)t * D];
+    const double m = cmn_block_sum(s, part) / (double)T;
+    double q = 0.0;
+    if (c < D)
+      for (int t = g; t < T; t += 4) {
+        const double d = (double)p[(size_t)t * D] - m;
+        q += d * d;
+      }
+    const double var = cmn_block_sum(q, part) / (double)(T - 1);  // T = 1: 0 / 0 = NaN, as torch.var
+    const double inv = 1.0 / sqrt(var + 1e-7);
+    if (c < D)
+      for (int t = g; t < T; t += 4) p[(size_t)t * D] = (float)((double)p[(size_t)t * D] * inv);
+  }
 }
 
 }  // namespace
@@ -288,7 +315,15 @@ void launch_layernorm(const LayerNormArgs& p, hipStream_t s) {
 
 void launch_cmn_rows(float* x, int B, int T, int D, hipStream_t s, const int* seg) {
   WSP_CHECK(B > 0 && (T > 0 || seg) && D > 0, "cmn: bad shape");
-  hipLaunchKernelGGL(cmn_rows_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, x, T, D, seg);
+  hipLaunchKernelGGL(cmn_rows_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, x, T, D, seg, 1);
+  WSP_HIP(hipGetLastError());
+}
+
+void launch_cmvn_rows(float* x, int B, int T, int D, int norm_mean, int norm_var, hipStream_t s, const int* seg) {
+  WSP_CHECK(B > 0 && (T > 0 || seg) && D > 0, "cmvn: bad shape");
+  const int mode = (norm_mean ? 1 : 0) | (norm_var ? 2 : 0);
+  if (!mode) return;
+  hipLaunchKernelGGL(cmn_rows_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, x, T, D, seg, mode);
   WSP_HIP(hipGetLastError());
 }
 

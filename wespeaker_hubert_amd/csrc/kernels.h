@@ -163,14 +163,37 @@ void launch_nhwc_to_tfc(const float* in, float* out, int B, int F, int T, int C,
 void launch_resnet_stem(const float* feats, int B, int T, int F, int C0, const float* w, const float* bias,
                         float* out, hipStream_t s);
 
-// Kaldi fbank (float64 arithmetic) + optional fused CMN.  `tables` = device
-// copy of fbank_tables().
-constexpr int kFbankTableDoubles = 1664 + 1024 + 1152;
-void fbank_tables(double* host_tab);  // window, twiddles, sparse mel filters
+// Kaldi fbank (float64 arithmetic) + optional fused CMN (fbank.hip).
+// torchaudio.compliance.kaldi.fbank options the extraction path passes
+// (processor.py:472-502, cli/speaker.py:89-104): bins, rate, frame length /
+// shift in ms, window; low / high mel edges (torchaudio defaults 20 / 0).
+struct FbankConfig {
+  int num_bins = 80, sample_rate = 16000, window = 0;  // window: WSP_WINDOW_*
+  double frame_length_ms = 25.0, frame_shift_ms = 10.0, low_freq = 20.0, high_freq = 0.0;
+  // derived (fbank_config_resolve): samples per frame / shift, padded FFT size
+  int frame_len = 0, frame_shift = 0, padded = 0;
+};
+// Validates `c` and fills frame_len / frame_shift / padded (torchaudio's
+// int(sr * ms * 0.001) and round_to_power_of_two); padded must be 256 or 512.
+void fbank_config_resolve(FbankConfig& c);
+// torchaudio get_mel_banks(num_bins, padded, sr, low, high) in its float32
+// arithmetic (correctly rounded log): w = [num_bins][padded / 2 + 1], the
+// Nyquist column 0 (kaldi.py pads it).  Computed here, at plan time.
+void fbank_mel_banks(const FbankConfig& c, std::vector<float>& w);
+// Device-side description of one configuration: table (window, twiddles,
+// lane-interleaved mel filters) + geometry.
+struct FbankPlan {
+  FbankConfig cfg;
+  bool fixed = false;  // the 80-bin 16 kHz 25 / 10 ms hamming instance (compile-time geometry)
+  int len0 = 0, len1 = 0;  // padded filter lengths of bins 0..63 / 64..
+  std::vector<double> host_tab;
+  const double* tab = nullptr;  // device copy (owned by the caller's cache)
+};
+void fbank_plan(const FbankConfig& c, FbankPlan& p);  // host part (table)
 // Segmented: wseg / fseg = device int32 [B+1] sample / frame offsets, T = frames
 // of the longest utterance (grid size); N, ld unused.
 void launch_fbank(const void* wav, int dtype, int B, int N, int ld, float scale, float* feats,
-                  int T, int cmn, const double* tables, hipStream_t s, const int* wseg = nullptr,
+                  int T, int cmn, const FbankPlan& plan, hipStream_t s, const int* wseg = nullptr,
                   const int* fseg = nullptr);
 
 // HuBERT-base front end (hubert.hip).
@@ -214,6 +237,11 @@ struct LayerNormArgs {
 void launch_layernorm(const LayerNormArgs& p, hipStream_t s);
 // x [B][T][D] -= mean over T  (apply_cmvn(norm_mean=True, norm_var=False))
 void launch_cmn_rows(float* x, int B, int T, int D, hipStream_t s, const int* seg = nullptr);
+// apply_cmvn(norm_mean, norm_var) (dataset_utils.py:19-26): x -= mean_T; then
+// x /= sqrt(var_T(unbiased) + 1e-7) — the variance about the (new) mean, so
+// norm_var alone on already mean-normalised rows equals the pair.
+void launch_cmvn_rows(float* x, int B, int T, int D, int norm_mean, int norm_var, hipStream_t s,
+                      const int* seg = nullptr);
 
 // Scoring helpers.
 void launch_l2_normalize(const float* x, const float* sub, float* y, int R, int D, hipStream_t s);

@@ -77,6 +77,135 @@ def _read_vector(f) -> np.ndarray:
     return np.frombuffer(f.read(n * np.dtype(dtype).itemsize), dtype=dtype).astype(dtype[1:])
 
 
+# --------------------------------------------------------------- matrices --
+# kaldiio.load_mat as the `feat` data type calls it (processor.parse_feat,
+# wespeaker/dataset/processor.py:171-196): "<ark path>:<byte offset>" (plus
+# kaldiio's optional "[r0:r1]" / "[r0:r1,c0:c1]" slice), or a path alone for the
+# first object in the file.  Kaldi's published binary layouts
+# (src/matrix/kaldi-matrix.cc Matrix::Read, src/matrix/compressed-matrix.{h,cc}):
+#   "\0B" "FM " | "DM "  '\x04' int32 rows  '\x04' int32 cols  rows*cols f32 | f64
+#   "\0B" "CM " | "CM2 " | "CM3 "  GlobalHeader {f32 min, f32 range, i32 rows, i32 cols}
+#       CM  (kOneByteWithColHeaders): cols x PerColHeader {u16 p0, p25, p75, p100},
+#           then rows bytes per column (column-major)
+#       CM2 (kTwoByte): rows*cols u16 row-major; CM3 (kOneByte): rows*cols u8 row-major
+# and the text form "[ v v v\n v v v ]".  Decoding follows CompressedMatrix::CopyToMat
+# in its float arithmetic.  Byte-exact parity with kaldiio is *unpinned* (kaldiio is
+# absent); tests/test_kaldi_io.py fixes the layouts from hand-written bytes.
+
+_U16_SCALE = np.float32(1.52590218966964e-05)  # compressed-matrix.cc Uint16ToFloat: 1/65535 as a float literal
+
+
+def _read_int32(f) -> int:
+    if f.read(1) != b"\x04":
+        raise ValueError("bad int32 size marker")
+    return struct.unpack("<i", f.read(4))[0]
+
+
+def _char_to_float(p0, p25, p75, p100, v: np.ndarray) -> np.ndarray:
+    """CompressedMatrix::CharToFloat: float products times a double reciprocal, rounded to float."""
+    v32 = v.astype(np.float32)
+    lo = (p0 + ((p25 - p0) * v32).astype(np.float64) * (1 / 64.0))
+    mid = (p25 + ((p75 - p25) * (v32 - np.float32(64))).astype(np.float64) * (1 / 128.0))
+    hi = (p75 + ((p100 - p75) * (v32 - np.float32(192))).astype(np.float64) * (1 / 63.0))
+    return np.where(v <= 64, lo, np.where(v <= 192, mid, hi)).astype(np.float32)
+
+
+def _read_compressed(f, fmt: bytes) -> np.ndarray:
+    mn, rng, rows, cols = struct.unpack("<ffii", f.read(16))
+    mn, rng = np.float32(mn), np.float32(rng)
+    if rows < 0 or cols < 0:
+        raise ValueError("bad compressed matrix header")
+    if fmt == b"CM":
+        hdr = np.frombuffer(f.read(8 * cols), dtype="<u2").reshape(cols, 4).astype(np.float32)
+        pct = (mn + rng * _U16_SCALE * hdr).astype(np.float32)  # Uint16ToFloat per percentile
+        data = np.frombuffer(f.read(rows * cols), dtype=np.uint8).reshape(cols, rows)
+        out = np.empty((rows, cols), dtype=np.float32)
+        for c in range(cols):
+            out[:, c] = _char_to_float(pct[c, 0], pct[c, 1], pct[c, 2], pct[c, 3], data[c])
+        return out
+    if fmt == b"CM2":
+        data = np.frombuffer(f.read(2 * rows * cols), dtype="<u2").reshape(rows, cols)
+        inc = np.float64(rng) * (1.0 / 65535.0)  # CopyToMat: increment = range * (1.0 / 65535.0)
+    elif fmt == b"CM3":
+        data = np.frombuffer(f.read(rows * cols), dtype=np.uint8).reshape(rows, cols)
+        inc = np.float64(rng) * (1.0 / 255.0)
+    else:
+        raise ValueError(f"unsupported compressed matrix type {fmt!r}")
+    inc = np.float32(inc)
+    return (mn + data.astype(np.float32) * inc).astype(np.float32)
+
+
+def _read_text_matrix(f, first: bytes) -> np.ndarray:
+    buf = first
+    while b"]" not in buf:
+        c = f.read(4096)
+        if not c:
+            raise ValueError("unterminated text matrix")
+        buf += c
+    body = buf[buf.index(b"[") + 1:buf.index(b"]")].decode("ascii")
+    rows = [ln.split() for ln in body.strip().splitlines() if ln.strip()]
+    if not rows:
+        return np.zeros((0, 0), dtype=np.float32)
+    return np.asarray([[float(v) for v in r] for r in rows], dtype=np.float32)
+
+
+def read_matrix(f) -> np.ndarray:
+    """One Kaldi matrix at the file position (binary FM / DM / CM / CM2 / CM3, or text)."""
+    head = f.read(2)
+    if head != b"\0B":
+        return _read_text_matrix(f, head)
+    tok = b""
+    while True:
+        c = f.read(1)
+        if not c:
+            raise ValueError("truncated kaldi token")
+        if c == b" ":
+            break
+        tok += c
+    if tok in (b"FM", b"DM"):
+        rows, cols = _read_int32(f), _read_int32(f)
+        dt = "<f4" if tok == b"FM" else "<f8"
+        n = rows * cols
+        arr = np.frombuffer(f.read(n * np.dtype(dt).itemsize), dtype=dt)
+        if arr.size != n:
+            raise ValueError("truncated kaldi matrix")
+        return arr.reshape(rows, cols).astype(dt[1:])
+    if tok in (b"CM", b"CM2", b"CM3"):
+        return _read_compressed(f, tok)
+    raise ValueError(f"unsupported kaldi matrix type {tok!r}")
+
+
+def _parse_slice(spec: str):
+    """kaldiio's trailing "[r0:r1]" / "[r0:r1,c0:c1]" range."""
+    if not spec.endswith("]") or "[" not in spec:
+        return spec, None
+    base, _, rng = spec[:-1].rpartition("[")
+    parts = []
+    for p in rng.split(","):
+        a, _, b = p.partition(":")
+        parts.append(slice(int(a) if a else None, int(b) if b else None))
+    return base, tuple(parts)
+
+
+def load_mat(spec: str) -> np.ndarray:
+    """kaldiio.load_mat for "<path>:<offset>[slice]" and "<path>" (first object)."""
+    spec, sl = _parse_slice(spec.strip())
+    path, off = spec, 0
+    head, sep, tail = spec.rpartition(":")
+    if sep and tail.isdigit() and head:
+        path, off = head, int(tail)
+    with open(path, "rb") as f:
+        f.seek(off)
+        if off == 0:  # an ark file from its start: "<key> " precedes the object
+            peek = f.read(2)
+            f.seek(0)
+            if peek not in (b"\0B",) and not peek.startswith(b"["):
+                while f.read(1) not in (b" ", b""):
+                    pass
+        mat = read_matrix(f)
+    return mat[sl] if sl is not None else mat
+
+
 def load_ark(path: str) -> Iterator[Tuple[str, np.ndarray]]:
     with open(path, "rb") as f:
         while True:
