@@ -315,14 +315,15 @@ def plumbing_main(args):
 
 def rccl_check(dev, world: int, rank: int) -> dict:
     """Runs wespeaker_hubert_amd.dist.allreduce_sums on device buffers (rank r adds
-    r + 1 to a [G, D] sum and its counts) and compares with the closed form."""
+    r + 1 to a [G, D] sum and its counts) and compares with the closed form (at world 1
+    too: the collective is forced, tests/test_gpu_rccl.py)."""
     import torch.distributed as tdist
     from wespeaker_hubert_amd.dist import allreduce_sums
     G, D = 1000, 192
     acc = torch.full((G, D), float(rank + 1), dtype=torch.float64, device=dev)
     cnt = torch.full((G,), float(rank + 1), dtype=torch.float64, device=dev)
     t = time.perf_counter()
-    allreduce_sums(acc, cnt)
+    allreduce_sums(acc, cnt, force=True)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     ms = (time.perf_counter() - t) * 1e3

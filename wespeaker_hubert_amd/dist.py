@@ -36,12 +36,13 @@ def shard_lines(lines: Sequence[str], rank: int, world_size: int) -> List[str]:
     return list(lines[lo:hi])
 
 
-def allreduce_sums(acc: torch.Tensor, cnt: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+def allreduce_sums(acc: torch.Tensor, cnt: torch.Tensor, force: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """In-place SUM all-reduce of per-group embedding sums [G, D] and counts [G]
-    (one fused buffer -> one collective)."""
+    (one fused buffer -> one collective).  A world of one returns at once unless
+    `force` (the hardware check of the RCCL path on a one-GPU box)."""
     if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
         return acc, cnt
-    if torch.distributed.get_world_size() == 1:
+    if torch.distributed.get_world_size() == 1 and not force:
         return acc, cnt
     buf = torch.cat([acc.reshape(-1), cnt.reshape(-1)]).to(torch.float64)
     if torch.distributed.get_backend() == "gloo":  # gloo reduces host tensors (CPU tests, 1-GPU rehearsal)
