@@ -211,7 +211,12 @@ int wsp_model_forward_segments(wsp_model* m, const float* feats, int B, const in
  *   "ln_fold"      HuBERT front end, x3_variant 7: 1 = the post-attention LayerNorm folded into
  *                  the GEMMs (out_proj emits per-row mean / M2 partials, fc1 runs on the
  *                  un-normalised rows with gamma in W, fc2 normalises its residual on the fly;
- *                  12 fewer launches per forward, measured neutral), 0 = LayerNorm kernels (default)
+ *                  12 fewer launches per forward, measured neutral), 0 = LayerNorm kernels (default).
+ *                  fc1's fold computes (W'u - mu colsum(W')) rstd: rows whose |mean| is far above
+ *                  their std cancel there (fp32), which is one reason it stays off by default
+ *   "tail_batch"   HuBERT front end: 1 = when the feature extractor runs in utterance chunks
+ *                  (conv0 output > 2 GiB), CNN layers 4-6 run once over the whole batch
+ *                  (default), 0 = per chunk; same per-row arithmetic, bit-identical rows
  *   "layer"        HuBERT front end only, before finalize: -1 = weighted sum of all
  *                  hidden states (default), k = hidden state k alone (s3prl.py:84-87)
  * Deprecated (accepted, mapped to the shipped kernels since r3 pruned the others):

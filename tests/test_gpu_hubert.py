@@ -111,6 +111,7 @@ def test_batch_rows_independent_and_chunked(sd_np):
     B, W = 60, 80000
     wav = torch.from_numpy(_wav(10, B, W)).to(DEV)
     fe = _frontend(sd_np)
+    fe.set_option("streams", 1)  # one utterance range: 60 x 15 999 conv0 rows > one 917 504-row chunk
     full = fe.extract(wav, cmn=True)
     for i in (0, 31, B - 1):
         one = fe.extract(wav[i:i + 1].contiguous(), cmn=True)
@@ -294,3 +295,32 @@ def test_layernorm_fold_matches_kernels_and_oracle(sd_np, sd_t, layer):
             else:
                 ref = hubert_ref.s3prl_upstream(torch.from_numpy(wavs[i][None]), sd_t)[layer][0]
         assert (a[offs[i]:offs[i + 1]] - ref).abs().max().item() <= FEAT_ATOL, i
+
+
+def test_ragged_multichunk_batch_tail_batch(sd_np):
+    """a ragged wsp_frontend_forward_segments batch big enough to split the feature
+    extractor into utterance chunks (conv0 rows above 2 GiB / 2 KB = 917 504 per chunk): CNN
+    layers 4-6 then run batch-wide over global level-3/4/5 offsets with each chunk's rows
+    placed at its chunk-relative row3.  Rows on both sides of the chunk boundary equal their
+    batch-of-one features, and tail_batch 1 equals tail_batch 0 (per chunk) bit for bit."""
+    rng = np.random.default_rng(3)
+    lens = [int(n) for n in rng.integers(40000, 120000, 76)]
+    wavs = [synth_audio(900 + i, 1, n, int16_scale=False)[0] for i, n in enumerate(lens)]
+    t0 = [(n - 10) // 5 + 1 for n in lens]
+    cap = (1 << 31) // 8 * 7 // (512 * 4)
+    rows, b1 = 0, 0
+    while b1 < len(lens) and (b1 == 0 or rows + t0[b1] <= cap):
+        rows += t0[b1]
+        b1 += 1
+    assert 0 < b1 < len(lens), "the batch must span two feature-extractor chunks"
+    fe = _frontend(sd_np)
+    fe.set_option("streams", 1)  # one utterance range, so the chunking above is the kernel's
+    feats, offs = fe.extract_segments([torch.from_numpy(w) for w in wavs], cmn=True)
+    assert fe.get_option("tail_batch") == 1
+    for i in (0, b1 - 1, b1, len(lens) - 1):
+        one = fe.extract(torch.from_numpy(wavs[i][None]).to(DEV), cmn=True)[0]
+        d = (feats[offs[i]:offs[i + 1]] - one).abs().max().item()
+        assert d <= 1e-5, f"row {i} (chunk boundary at {b1}): {d}"
+    fe.set_option("tail_batch", 0)
+    feats0, offs0 = fe.extract_segments([torch.from_numpy(w) for w in wavs], cmn=True)
+    assert offs0 == offs and torch.equal(feats0, feats)

@@ -198,7 +198,7 @@ __device__ __forceinline__ void g_epilogue_rows(const ConvGemmArgs& p, f32x4 (&a
         pm2[u] = q2;
       }
     }
-    if constexpr ((LNM & 1) != 0) {  // merge the half-wave's 32 lanes per row; lanes 0 / 32 store
+    if constexpr ((LNM & 1) != 0) {  // merge the half-wave's 32 lanes per row; lanes 16 / 48 store
       g_ln_pieces<16>(pm, pm2);
       if ((lane & 31) == 16) {
 #pragma unroll

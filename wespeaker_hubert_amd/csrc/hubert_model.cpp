@@ -239,7 +239,7 @@ HubertPlan Model::Impl::hubert_plan(int B, const int* lens) const {
   pl.maxT6 = *std::max_element(T[6].begin(), T[6].end());
   // layers 4..6 batch-wide: more than one chunk, level-3 rows within a 2 GiB operand, and the
   // chunk buffers (free after the chunk loop) large enough for the level-4 / level-5 rows
-  pl.tail_batch = pl.chunks.size() > 1 && pl.M3 * kConvDim * sizeof(float) < ((size_t)1 << 31) / 8 * 7 &&
+  pl.tail_batch = tail_batch && pl.chunks.size() > 1 && pl.M3 * kConvDim * sizeof(float) < ((size_t)1 << 31) / 8 * 7 &&
                   pl.M4 <= pl.maxA && pl.M5 <= pl.maxB;
   WSP_CHECK(pl.M * kFfn * sizeof(float) < ((size_t)1 << 31) - 64,
             "HuBERT batch too large for one call (frames * 3072 floats must stay below 2 GiB)");

@@ -128,6 +128,8 @@ struct SmallLinearArgs {
   size_t scratch_floats = 0;
 };
 void launch_small_linear(const SmallLinearArgs& p, hipStream_t s);
+// scratch floats the split-K path needs (0 below K = 4096); offering less is an error
+size_t small_linear_scratch_floats(int R, int N, int K);
 
 // Segmented (ragged) batches: `seg` = device int32 [B+1] row offsets, utterance
 // b owning rows [seg[b], seg[b+1]); null = uniform rows b*T .. b*T + T-1.

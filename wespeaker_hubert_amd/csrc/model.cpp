@@ -255,6 +255,9 @@ void Model::set_option(const std::string& key, int value) {
   } else if (key == "ln_fold") {
     WSP_CHECK(value == 0 || value == 1, "ln_fold must be 0 (LayerNorm kernels) or 1 (folded into the GEMMs)");
     impl->ln_fold = value;
+  } else if (key == "tail_batch") {
+    WSP_CHECK(value == 0 || value == 1, "tail_batch must be 0 (CNN layers 4-6 per chunk) or 1 (batch-wide)");
+    impl->tail_batch = value;
   } else if (key == "astp_fused") {
     WSP_CHECK(value >= 0 && value <= 3, "astp_fused must be 0 (linear2 GEMM + pooling kernel) or 1 (fused)");
     impl->astp_fused_on = value ? 1 : 0;  // 2 / 3: former fused variants (r3 pruned), deprecated aliases of 1
@@ -296,6 +299,7 @@ int Model::get_option(const std::string& key) const {
   if (key == "attn_pipe") return m.attn_pipe;
   if (key == "pos_conv") return m.pos_conv;
   if (key == "ln_fold") return m.ln_fold;
+  if (key == "tail_batch") return m.tail_batch;
   if (key == "res2_variant") return m.res2_variant;
   if (key == "x3_variant") return m.x3_variant;
   if (key == "conv3x3_img") return m.conv3x3_img_on;

@@ -220,6 +220,9 @@ struct Model::Impl {
   // HuBERT: 1 = the post-attention LayerNorm folded into out_proj / fc1 / fc2 (x3_variant 7); measured
   // neutral on C4 (A/B 4 234 / 4 223 vs 4 233 / 4 232 emb/s, profiles/r5g_ln_fold.txt): default off
   int ln_fold = 0;
+  // HuBERT CNN layers 4-6 once over the whole batch when the feature extractor runs in several
+  // utterance chunks (r5); 0 = per chunk (the tests compare the two)
+  int tail_batch = 1;
   void build_hubert_params();
   void finalize_hubert();
   int hubert_cnn_frames(int N, int upto) const;

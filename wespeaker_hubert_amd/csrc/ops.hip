@@ -121,6 +121,12 @@ __global__ __launch_bounds__(256) void small_linear_reduce_kernel(const SmallLin
 }
 }  // namespace
 
+size_t small_linear_scratch_floats(int R, int N, int K) {
+  if (K < 4096) return 0;
+  const int kslice = std::max(256, (ceil_div(K, 32) + 63) / 64 * 64);
+  return (size_t)ceil_div(K, kslice) * R * N;
+}
+
 void launch_small_linear(const SmallLinearArgs& p, hipStream_t s) {
   if (p.R == 0) return;
   const int rb = ceil_div(p.R, kSKR), nb = ceil_div(p.N, 64);
@@ -129,13 +135,15 @@ void launch_small_linear(const SmallLinearArgs& p, hipStream_t s) {
   if (p.scratch && p.K >= 4096) {
     const int kslice = std::max(256, (ceil_div(p.K, 32) + 63) / 64 * 64);
     const int nks = ceil_div(p.K, kslice);
-    if ((size_t)nks * p.R * p.N <= p.scratch_floats) {
-      hipLaunchKernelGGL(small_linear_splitk_kernel, dim3(rb, nb, nks), dim3(64 * kSW), 0, s, p, kslice);
-      WSP_HIP(hipGetLastError());
-      hipLaunchKernelGGL(small_linear_reduce_kernel, dim3(ceil_div(p.R * p.N, 256)), dim3(256), 0, s, p, nks);
-      WSP_HIP(hipGetLastError());
-      return;
-    }
+    // a caller offering scratch must offer enough (small_linear_scratch_floats): falling back to
+    // the one-pass kernel would sum in another order, and a batch would no longer equal its
+    // batch-of-one rows
+    WSP_CHECK((size_t)nks * p.R * p.N <= p.scratch_floats, "small_linear: split-K scratch too small");
+    hipLaunchKernelGGL(small_linear_splitk_kernel, dim3(rb, nb, nks), dim3(64 * kSW), 0, s, p, kslice);
+    WSP_HIP(hipGetLastError());
+    hipLaunchKernelGGL(small_linear_reduce_kernel, dim3(ceil_div(p.R * p.N, 256)), dim3(256), 0, s, p, nks);
+    WSP_HIP(hipGetLastError());
+    return;
   }
   dim3 grid(ceil_div(p.R, kRB), ceil_div(p.N, 64));
   hipLaunchKernelGGL(small_linear_kernel, grid, dim3(64 * kSW), 0, s, p);
