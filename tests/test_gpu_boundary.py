@@ -222,7 +222,11 @@ def test_extract_driver_sre_8k_64bin_resnet_norm_var(tmp_path):
 
 
 def test_extract_driver_cmvn_false(tmp_path):
-    """dataset_args.cmvn: false — features go to the backbone unnormalised."""
+    """dataset_args.cmvn: false — features go to the backbone unnormalised.  No reference
+    recipe uses it; with raw log-mels (mean ~10-15) and synthetic weights (whose BN running
+    statistics do not absorb that offset) every activation and the embedding itself come out
+    ~10x larger than on CMN'd input, so the per-dim bar is taken relative to the embedding's
+    largest magnitude (1e-4 x max(1, max|ref|)); cosine >= 0.9999 as everywhere."""
     from wespeaker_hubert_amd.bin.extract import extract
     arch = "ECAPA_TDNN_c512"
     sd = _make_model_dir(tmp_path, arch, {"feat_dim": 40, "embed_dim": 192, "pooling_func": "ASTP"},
@@ -242,7 +246,11 @@ def test_extract_driver_cmvn_false(tmp_path):
         f = fbank_ref.fbank(pcm[i], 40)[None]
         with torch.no_grad():
             _, ref = models_ref.forward(arch, torch.from_numpy(f), sd)
-        _assert_emb(got[f"c{i}"], ref[0].numpy())
+        ref = ref[0].numpy()
+        g = got[f"c{i}"]
+        assert np.all(np.isfinite(g)) and _cos(g, ref) >= 0.9999
+        assert np.abs(g - ref).max() < 1e-4 * max(1.0, float(np.abs(ref).max())), (np.abs(g - ref).max(),
+                                                                                    np.abs(ref).max())
 
 
 @pytest.mark.parametrize("win", ["povey", "blackman"])
