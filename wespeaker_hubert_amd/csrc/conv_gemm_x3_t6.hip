@@ -308,7 +308,10 @@ __device__ __forceinline__ void g_epilogue_cs(const ConvGemmArgs& p, f32x4 (&acc
   }
 }
 
-template <int AM, bool CSK, int LNM = 0>
+// XP: development experiments (tools/gemm_check built with -DWSP_G7_XP; the library instantiates
+// XP = 0 only): 1 = timing-only, the A fragments bit-reinterpreted instead of split (no split
+// VALU; wrong results); 2 = the next tile's DMA pieces interleaved into the quarters
+template <int AM, bool CSK, int LNM = 0, int XP = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, const __bf16* __restrict__ whi,
                                                       const __bf16* __restrict__ wlo) {
   using L = Lds<true, 16>;
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
   const __amdgpu_buffer_rsrc_t rwl = make_rsrc(wlo);
   const int nk = p.Kp / BK;  // >= 2 (Kp % 64 == 0)
   int jt = 0, ct = 0;  // tap and channel of the next k-tile to fetch (k-tiles are fetched in order)
-  auto dma = [&](int kt, int buf) {
+  auto dma = [&](int kt, int buf, int part = 3) {  // part bit 0: A pieces, bit 1: W pieces
     unsigned char* st = smem + buf * kGStage;
     const int off = jt * p.dil - p.pad;
     const float* base = p.a[0];
@@ -380,6 +383,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
     const __amdgpu_buffer_rsrc_t ra = make_rsrc(base);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      if (!(part & 1)) break;
       if constexpr (DENSE) {
         g_dma(ra, st + (4 * wave + i) * 1024, a_r[i] >= 0 ? (a_r[i] * ld + cl + (i & 1 ? ac1 : ac0)) * 4 : kOOB);
       } else if constexpr (AM == 2) {
@@ -397,10 +401,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      if (!(part & 2)) break;
       const int o = woff[i] + kt * 64;
       g_dma(rwh, st + kGA + (2 * wave + i) * 1024, o);
       g_dma(rwl, st + kGA + kGW + (2 * wave + i) * 1024, o);
     }
+    if (!(part & 2)) return;  // the tap / channel cursor advances with the W half (issued last)
     ct += 32;
     if (ct >= p.cin) {
       ct -= p.cin;
@@ -422,6 +428,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
       const int r = wm * 64 + (ih * 2 + i) * 16 + r16;
       const f32x4 x0 = *reinterpret_cast<const f32x4*>(st + g_aslot(r, 2 * qk));
       const f32x4 x1 = *reinterpret_cast<const f32x4*>(st + g_aslot(r, 2 * qk + 1));
+      if constexpr (XP == 1) {
+        ah[i] = __builtin_bit_cast(bf16x8, x0);
+        al[i] = __builtin_bit_cast(bf16x8, x1);
+        continue;
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const __bf16 h0 = (__bf16)x0[e], h1 = (__bf16)x1[e];
@@ -460,9 +471,34 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
   dma(1, 1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0 landed (8 DMAs per k-tile and lane)
   __builtin_amdgcn_s_barrier();
+  // (XP 2 keeps this prologue: tile 1 is in flight, iteration 0 issues nothing, iteration kt >= 1
+  // issues tile kt + 1 into the buffer tile kt - 1 left)
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     const unsigned char* st = smem + buf * kGStage;
+    if constexpr (XP == 2) {
+      // the next tile's pieces go out between this tile's quarters (the other buffer is free:
+      // every wave passed the barrier that ended tile kt - 1's reads of it)
+      rdA(st, 0);
+      rdB(st, 0);
+      mm(0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt >= 1 && kt + 1 < nk) dma(kt + 1, buf ^ 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      rdB(st, 1);
+      mm(0, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt >= 1 && kt + 1 < nk) dma(kt + 1, buf ^ 1, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      rdA(st, 1);
+      mm(1, 1);
+      rdB(st, 0);
+      mm(1, 0);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      continue;
+    }
     // family 6's snake over the four 2 x 4 quarters of the 64 x 128 wave tile
     rdA(st, 0);
     rdB(st, 0);
@@ -562,6 +598,28 @@ void t_g256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t
     hipLaunchKernelGGL((conv_gemm_g<2, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
   WSP_HIP(hipGetLastError());
 }
+
+#ifdef WSP_G7_XP
+// development entry (tools/gemm_check): plain family 7 operand forms (no LayerNorm fold)
+void t_g256_xp(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s, int xp) {
+  const int nwg = ((p.M + 255) / 256) * (p.N / 256);
+  constexpr int lds0 = 2 * kGStage > kGEpiBytes ? 2 * kGStage : kGEpiBytes;
+  constexpr int lds = lds0 > kGCsBytes ? lds0 : kGCsBytes;
+  const bool dense = p.taps == 1 && p.pad == 0 && p.stride == 1 && !p.iseg && (p.seg || p.Ti == p.T);
+  const int am = !uniform_ktiles(p) ? 2 : dense ? 1 : 0;
+  WSP_CHECK(am != 2 && !p.lnmode, "t_g256_xp: AM 0 / 1 only");
+#define WSP_XPL(AMv, CS, XPv) hipLaunchKernelGGL((conv_gemm_g<AMv, CS, 0, XPv>), dim3(nwg), dim3(512), lds, s, p, h, l)
+  if (xp == 1) {
+    if (p.colsum) { if (am == 1) WSP_XPL(1, true, 1); else WSP_XPL(0, true, 1); }
+    else { if (am == 1) WSP_XPL(1, false, 1); else WSP_XPL(0, false, 1); }
+  } else {
+    if (p.colsum) { if (am == 1) WSP_XPL(1, true, 2); else WSP_XPL(0, true, 2); }
+    else { if (am == 1) WSP_XPL(1, false, 2); else WSP_XPL(0, false, 2); }
+  }
+#undef WSP_XPL
+  WSP_HIP(hipGetLastError());
+}
+#endif
 
 }  // namespace x3
 }  // namespace wsp
