@@ -519,19 +519,24 @@ __global__ __launch_bounds__(FB* TB * 2 * WN, MINB) void bottleneck_tail_kernel(
 // (interleaved model-level A/B).
 
 // dynamic LDS of tail2_kernel: the patch image, later y2 fragments + the chunk buffer
+// FB: position runs (frequency rows) per block — 2 / 4 / 8 for 128 / 64 / 32 planes, or 1 for
+// 128 planes (r6: one run per block, 51 KB, three blocks per CU)
 template <int C>
+constexpr int tail2_fb() { return C == 128 ? 2 : C == 64 ? 4 : 8; }
+template <int C, int FB = tail2_fb<C>()>
 constexpr int tail2_lds() {
-  constexpr int FB = C == 128 ? 2 : C == 64 ? 4 : 8, GW = 4 / (FB / 2);
+  constexpr int RW = FB >= 2 ? 2 : 1, GW = 4 * RW / FB;
   constexpr int cbp = FB * 32 * GW * 64, need = FB * (C / 16) * 2048 + cbp + 64 + cbp;
   return Img<C, FB, 32>::LDS > need ? Img<C, FB, 32>::LDS : need;
 }
 
-template <int C, int P1, int RD3, int RD1>
-__global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs p) {
-  constexpr int FB = C == 128 ? 2 : C == 64 ? 4 : 8, TB = 32;
+template <int C, int P1, int RD3, int RD1, int FB = tail2_fb<C>(), int MINB = 2>
+__global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailArgs p) {
+  constexpr int TB = 32;
   using G = Img<C, FB, TB, 1, 4>;  // patch image staged by the 4 waves
   constexpr int PT = G::PT, CT = G::CT, KS = G::KS;
-  constexpr int NR = FB, GW = 4 / (NR / 2);      // runs; column groups per run pair
+  // runs; runs per wave (a pair, or the block's one run); column groups per wave's runs
+  constexpr int NR = FB, RW = NR >= 2 ? 2 : 1, GW = 4 * RW / NR;
   constexpr int C4 = 4 * C, NT3 = C4 / 32, KS3 = C / 16, NT1 = C / 32;
   constexpr int NCHK = NT3 / GW, KB = 2 * GW;    // chunks of GW tiles; conv1 k-steps per chunk
   constexpr int Y2B = NR * KS3 * 2048;           // y2 fragments of every run
@@ -549,7 +554,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = tid >> 6;
-  const int pp = w / GW, g = w - pp * GW;  // run pair (runs 2 pp, 2 pp + 1), column group
+  const int pp = w / GW, g = w - pp * GW;  // run group (runs RW pp .. RW pp + RW - 1), column group
   const int r32 = lane & 31;
   const int h = lane >> 5;
   const int ntf = (p.F + FB - 1) / FB, ntt = (p.T + TB - 1) / TB;
@@ -572,18 +577,18 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.out + obase);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res + obase);
   const int tw = t0 + 4 * h;  // time of register 0
-  const int fw = f0 + 2 * pp;  // frequency row of the wave's first run
+  const int fw = f0 + RW * pp;  // frequency row of the wave's first run
   auto roff = [&](int i, int col, int r) {
     const int t = tw + (r & 3) + 8 * (r >> 2);
     return fw + i < p.F && t < p.T ? (((fw + i) * p.T + t) * C4 + col) * 4 : kOOB;
   };
-  float rv[2][16], b3v;
+  float rv[RW][16], b3v;
   const __amdgpu_buffer_rsrc_t rb3 = make_rsrc(p.b3);
   auto rload = [&](int c, bool live) {  // !live: the same loads, out of range (branch-free count)
     const int col = (GW * c + g) * 32 + r32;
     b3v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb3, live ? col * 4 : kOOB, 0, 0));
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RW; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         rv[i][r] = __builtin_bit_cast(
@@ -597,31 +602,31 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
     bh = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, o, 0, 0));
     bl = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, o + CT * 1024, 0, 0));
   };
-  auto read_b = [&](int kg, bf16x8 (&xh)[2], bf16x8 (&xl)[2]) {
+  auto read_b = [&](int kg, bf16x8 (&xh)[RW], bf16x8 (&xl)[RW]) {
     const int tap = kg / G::KC, cb = kg - tap * G::KC;
     const int kf = tap / 3, kt = tap - kf * 3;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int a = G::addr((2 * pp + i) * PT + r32 + kf * PT + kt, 2 * cb + h);
+    for (int i = 0; i < RW; ++i) {
+      const int a = G::addr((RW * pp + i) * PT + r32 + kf * PT + kt, 2 * cb + h);
       xh[i] = *reinterpret_cast<const bf16x8*>(xhi + a);
       xl[i] = *reinterpret_cast<const bf16x8*>(xlo + a);
     }
   };
-  f32x16 acc[2];
+  f32x16 acc[RW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < RW; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
-  auto mma_t = [&](const bf16x8 (&xh)[2], const bf16x8 (&xl)[2], const bf16x8& bh, const bf16x8& bl) {
+  auto mma_t = [&](const bf16x8 (&xh)[RW], const bf16x8 (&xl)[RW], const bf16x8& bh, const bf16x8& bl) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < RW; ++i) {
       acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, xl[i], acc[i], 0, 0, 0);
       acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl, xh[i], acc[i], 0, 0, 0);
       acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, xh[i], acc[i], 0, 0, 0);
     }
   };
   {
-    bf16x8 wh[P1], wl[P1], xh[2][2], xl[2][2];
+    bf16x8 wh[P1], wl[P1], xh[2][RW], xl[2][RW];
 #pragma unroll
     for (int d = 0; d < P1; ++d) wload(d, wh[d], wl[d]);
     __syncthreads();  // image complete
@@ -675,7 +680,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
   // registers 8 s2 .. 8 s2 + 7 of channel tile g)
   __syncthreads();  // every wave is done reading the image
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < RW; ++i)
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       bf16x8 vh, vl;
@@ -687,7 +692,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
         vh[e] = hh;
         vl[e] = (__bf16)(y - (float)hh);
       }
-      const int o = (((2 * pp + i) * KS3 + 2 * g + s2) * 2) * 1024 + lane * 16;
+      const int o = (((RW * pp + i) * KS3 + 2 * g + s2) * 2) * 1024 + lane * 16;
       *reinterpret_cast<bf16x8*>(y2s + o) = vh;
       *reinterpret_cast<bf16x8*>(y2s + o + 1024) = vl;
     }
@@ -704,10 +709,10 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
   sync();
   WSP_TAIL_STAMP(3);
 
-  auto read_y2 = [&](int ks, bf16x8 (&ah)[2], bf16x8 (&al)[2]) {
+  auto read_y2 = [&](int ks, bf16x8 (&ah)[RW], bf16x8 (&al)[RW]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int o = (((2 * pp + i) * KS3 + ks) * 2) * 1024 + lane * 16;
+    for (int i = 0; i < RW; ++i) {
+      const int o = (((RW * pp + i) * KS3 + ks) * 2) * 1024 + lane * 16;
       ah[i] = *reinterpret_cast<const bf16x8*>(y2s + o);
       al[i] = *reinterpret_cast<const bf16x8*>(y2s + o + 1024);
     }
@@ -717,27 +722,27 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
   auto cbaddr = [](int row, int c16) {
     return row * CBR + ((c16 ^ (CBR == 256 ? row & 15 : CBR == 128 ? (row >> 1) & 7 : (row >> 2) & 3)) << 4);
   };
-  auto read_cb = [&](int kk, bf16x8 (&ah)[2], bf16x8 (&al)[2]) {
+  auto read_cb = [&](int kk, bf16x8 (&ah)[RW], bf16x8 (&al)[RW]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int a = cbaddr((2 * pp + i) * 32 + r32, 2 * kk + h);
+    for (int i = 0; i < RW; ++i) {
+      const int a = cbaddr((RW * pp + i) * 32 + r32, 2 * kk + h);
       ah[i] = *reinterpret_cast<const bf16x8*>(cbhi + a);
       al[i] = *reinterpret_cast<const bf16x8*>(cblo + a);
     }
   };
-  auto mma2 = [](f32x16 (&d)[2], const bf16x8 (&ah)[2], const bf16x8 (&al)[2], const bf16x8& bh,
+  auto mma2 = [](f32x16 (&d)[RW], const bf16x8 (&ah)[RW], const bf16x8 (&al)[RW], const bf16x8& bh,
                  const bf16x8& bl) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < RW; ++i) {
       d[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, d[i], 0, 0, 0);
       d[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, d[i], 0, 0, 0);
       d[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, d[i], 0, 0, 0);
     }
   };
 
-  f32x16 acc1[2], a3[2];
+  f32x16 acc1[RW], a3[RW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < RW; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc1[i][r] = 0.f;
 #pragma unroll 1
@@ -746,10 +751,10 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
     for (int j = 0; j < RD1; ++j) w1load(KB * c + j, uh_[j], ul_[j]);  // land during the chunk's conv3
     // conv3, column tile GW c + g, the wave's two runs
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RW; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) a3[i][r] = 0.f;
-    bf16x8 ah[2][2], al[2][2];
+    bf16x8 ah[2][RW], al[2][RW];
     read_y2(0, ah[0], al[0]);
 #pragma unroll
     for (int q = 0; q < KS3; ++q) {
@@ -767,7 +772,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
     {
       const int col = (GW * c + g) * 32 + r32;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < RW; ++i) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float y = fmaxf(a3[i][r] + b3v + rv[i][r], 0.f);
@@ -780,7 +785,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
           const unsigned short lb = __builtin_bit_cast(unsigned short, ll);
           const unsigned send = (lane & 1) ? hb : lb;
           const unsigned recv = (unsigned)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
-          const int row = (2 * pp + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int row = (RW * pp + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           const int cc = g * 32 + (r32 & ~1);
           const int a = cbaddr(row, cc >> 3) + (cc & 7) * 2;
           if (lane & 1)
@@ -810,7 +815,7 @@ __global__ __launch_bounds__(256, 2) void tail2_kernel(const BottleneckTailArgs 
     const int col = g * 32 + r32;
     const float bv = p.b1n[col];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RW; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int t = tw + (r & 3) + 8 * (r >> 2);
@@ -866,11 +871,10 @@ void launch_tail_k(const BottleneckTailArgs& p, hipStream_t s) {
   hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB, NC, P1, PM>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
 }
 
-template <int C, int P1, int RD3, int RD1>
+template <int C, int P1, int RD3, int RD1, int FB = tail2_fb<C>(), int MINB = 2>
 void launch_tail2(const BottleneckTailArgs& p, hipStream_t s) {
-  constexpr int FB = C == 128 ? 2 : C == 64 ? 4 : 8;
   const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + 31) / 32);
-  hipLaunchKernelGGL((tail2_kernel<C, P1, RD3, RD1>), dim3(nblk), dim3(256), tail2_lds<C>(), s, p);
+  hipLaunchKernelGGL((tail2_kernel<C, P1, RD3, RD1, FB, MINB>), dim3(nblk), dim3(256), (tail2_lds<C, FB>()), s, p);
 }
 }  // namespace
 
