@@ -9,7 +9,9 @@
 //   gemm_check [case|all] [reps] [variants, e.g. 67]
 // r6 experiment variants: 8 = family 7 with the A split replaced by a bit reinterpretation
 // (timing only: no split VALU, same LDS / DMA traffic; its outputs differ), 9 = family 7 with the
-// next tile's DMA pieces interleaved into the k-tile's quarters (bit-identical).
+// next tile's DMA pieces interleaved into the k-tile's quarters (bit-identical); 10 = family 7's
+// LDS -> split -> MFMA loop alone (no DMA, no barrier in the k-loop; timing only); 11 = 10 without
+// the split (LDS -> MFMA alone; timing only).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -160,7 +162,7 @@ void run(const Case& c, int v, float* out, double* cs, hipStream_t s) {
   q.out = out;
   q.colsum = cs;
   if (v == 6) x3::t_4x2_2x4_mf16(q, c.whi, c.wlo, s);
-  else if (v == 8 || v == 9) x3::t_g256_xp(q, c.whi, c.wlo, s, v - 7);  // r6 experiments (8: timing only)
+  else if (v >= 8) x3::t_g256_xp(q, c.whi, c.wlo, s, v == 8 ? 1 : v == 9 ? 2 : v - 7);  // r6 experiments
   else {
     if (!x3::g256_supported(q)) { std::fprintf(stderr, "%s: family %d does not take these operands\n", c.name.c_str(), v); std::exit(2); }
     x3::t_g256(q, c.whi, c.wlo, s);
@@ -173,7 +175,7 @@ int main(int argc, char** argv) {
   const int reps = argc > 2 ? std::atoi(argv[2]) : 10;
   const std::string vs = argc > 3 ? argv[3] : "67";
   std::vector<int> vars;
-  for (char ch : vs) vars.push_back(ch - '0');
+  for (char ch : vs) vars.push_back(ch >= 'a' ? ch - 'a' + 10 : ch - '0');  // 'a' = 10, 'b' = 11
   const std::vector<int> ragged = {300, 257, 511, 123, 800, 6};
   std::vector<Case> cases;
   auto want = [&](const char* n) { return which == "all" || which == n; };
@@ -199,8 +201,8 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   int bad = 0;
   for (const Case& c : cases) {
-    std::vector<float*> out(10, nullptr);
-    std::vector<double*> cs(10, nullptr);
+    std::vector<float*> out(12, nullptr);
+    std::vector<double*> cs(12, nullptr);
     for (int v : vars) {
       CK(hipMalloc(&out[v], c.out_words * 4));
       CK(hipMemset(out[v], 0xff, c.out_words * 4));
@@ -214,7 +216,7 @@ int main(int argc, char** argv) {
       const unsigned long long dc = c.cs_words ? ndiff(cs[vars[0]], cs[v], c.cs_words) : 0;
       std::printf("%-10s family %d vs %d: %llu of %zu outputs differ, %llu column-sum words differ\n", c.name.c_str(), v,
                   vars[0], d, c.out_words, dc);
-      bad += (d != 0 || dc != 0) && v != 8;  // variant 8 is timing-only
+      bad += (d != 0 || dc != 0) && v != 8 && v < 10;  // variants 8, 10, 11 are timing-only
     }
     for (int round = 0; round < 3; ++round)
       for (int v : vars) {

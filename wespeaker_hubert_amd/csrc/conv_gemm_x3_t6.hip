@@ -310,7 +310,9 @@ __device__ __forceinline__ void g_epilogue_cs(const ConvGemmArgs& p, f32x4 (&acc
 
 // XP: development experiments (tools/gemm_check built with -DWSP_G7_XP; the library instantiates
 // XP = 0 only): 1 = timing-only, the A fragments bit-reinterpreted instead of split (no split
-// VALU; wrong results); 2 = the next tile's DMA pieces interleaved into the quarters
+// VALU; wrong results); 2 = the next tile's DMA pieces interleaved into the quarters; 3 = timing-
+// only, no DMA and no barrier inside the k-loop (every k-tile re-reads the two staged tiles: the
+// LDS -> split -> MFMA loop alone); 4 = 3 without the split (LDS -> MFMA alone)
 template <int AM, bool CSK, int LNM = 0, int XP = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, const __bf16* __restrict__ whi,
                                                       const __bf16* __restrict__ wlo) {
@@ -428,7 +430,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
       const int r = wm * 64 + (ih * 2 + i) * 16 + r16;
       const f32x4 x0 = *reinterpret_cast<const f32x4*>(st + g_aslot(r, 2 * qk));
       const f32x4 x1 = *reinterpret_cast<const f32x4*>(st + g_aslot(r, 2 * qk + 1));
-      if constexpr (XP == 1) {
+      if constexpr (XP == 1 || XP == 4) {
         ah[i] = __builtin_bit_cast(bf16x8, x0);
         al[i] = __builtin_bit_cast(bf16x8, x1);
         continue;
@@ -509,6 +511,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
     mm(1, 1);
     rdB(st, 0);
     mm(1, 0);
+    if constexpr (XP >= 3) {  // timing-only: the staged tiles are re-read, nothing is waited for
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      continue;
+    }
     // tile kt + 1 (issued a k-tile ago) has landed and every wave is done reading this half
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -612,6 +618,12 @@ void t_g256_xp(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStrea
   if (xp == 1) {
     if (p.colsum) { if (am == 1) WSP_XPL(1, true, 1); else WSP_XPL(0, true, 1); }
     else { if (am == 1) WSP_XPL(1, false, 1); else WSP_XPL(0, false, 1); }
+  } else if (xp == 3) {
+    WSP_CHECK(am == 1 && !p.colsum, "t_g256_xp 3: dense, no column sums");
+    WSP_XPL(1, false, 3);
+  } else if (xp == 4) {
+    WSP_CHECK(am == 1 && !p.colsum, "t_g256_xp 4: dense, no column sums");
+    WSP_XPL(1, false, 4);
   } else {
     if (p.colsum) { if (am == 1) WSP_XPL(1, true, 2); else WSP_XPL(0, true, 2); }
     else { if (am == 1) WSP_XPL(1, false, 2); else WSP_XPL(0, false, 2); }
