@@ -57,7 +57,9 @@ int main(int argc, char** argv) {
     for (const auto& w : waves) {
       int sr = 0;
       std::vector<int16_t> pcm = wespeaker::ReadWavPcm16(w.second, &sr);
-      if (sr != 16000) throw std::runtime_error(w.second + ": sample rate must be 16000");
+      // extract_emb_main.cc:52 CHECK_EQs 16000; here the engine's --sample_rate (default 16000)
+      if (sr != f.integer("sample_rate", 16000))
+        throw std::runtime_error(w.second + ": sample rate differs from --sample_rate");
       std::vector<float> emb;
       const auto t0 = std::chrono::steady_clock::now();
       engine.ExtractEmbedding(pcm.data(), (int)pcm.size(), &emb);

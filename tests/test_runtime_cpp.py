@@ -130,3 +130,43 @@ def test_gpu_extract_emb_main_matches_engine_oracle(exported, spc):
     score = float(r.stdout.split("Cosine score:")[1].split()[0])
     a, b = got["mid"], got["long"]
     assert abs(score - (a @ b / np.linalg.norm(a) / np.linalg.norm(b) + 1) / 2) < 1e-5
+
+
+@pytest.mark.gpu
+def test_gpu_engine_8k_64bin(tmp_path):
+    """FeaturePipelineConfig(num_bins, sample_rate) beyond 80 / 16 kHz (feature_pipeline.h:35-39:
+    25 / 10 ms frames at the given rate): --fbank_dim 64 --sample_rate 8000 with a 64-dim model,
+    chunked like speaker_engine.cc, against the oracle chain at 8 kHz."""
+    from oracle import fbank_ref, models_ref
+    from wespeaker_hubert_amd import arch as A
+    from wespeaker_hubert_amd.audio import write_wav
+    from wespeaker_hubert_amd.bin.export_hip import export
+    from wespeaker_hubert_amd.synthetic import synth_audio, synth_state_dict
+    _need_bins()
+    sd = synth_state_dict(52, A.param_list(A.make_spec(ARCH, feat_dim=64, embed_dim=192)))
+    torch.save({k: torch.from_numpy(v) for k, v in sd.items()}, tmp_path / "avg_model.pt")
+    with open(tmp_path / "config.yaml", "w") as f:
+        yaml.safe_dump({"model": ARCH, "model_args": {"feat_dim": 64, "embed_dim": 192}}, f)
+    path = export(str(tmp_path / "config.yaml"), str(tmp_path / "avg_model.pt"), str(tmp_path / "m.safetensors"))
+    pcm = synth_audio(711, 1, 21000)
+    write_wav(str(tmp_path / "a.wav"), pcm, sample_rate=8000)
+    (tmp_path / "wav.scp").write_text(f"a {tmp_path / 'a.wav'}\n")
+    spc = 16000
+    r = subprocess.run([os.path.join(BIN, "extract_emb_main"), "--speaker_model_path", path, "--wav_scp",
+                        str(tmp_path / "wav.scp"), "--result", str(tmp_path / "e.txt"), "--samples_per_chunk",
+                        str(spc), "--fbank_dim", "64", "--sample_rate", "8000"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    e = np.array([float(v) for v in (tmp_path / "e.txt").read_text().split()[1:]], dtype=np.float64)
+    fb = fbank_ref.fbank(pcm[0], 64, sample_freq=8000.0).astype(np.float32)
+    n = 1 + (spc - 200) // 80
+    chunks = [fb[t:t + n] for t in range(0, fb.shape[0] - n + 1, n)]
+    tail = fb[len(chunks) * n:]
+    if len(tail):
+        chunks.append(np.concatenate([tail, chunks[0][:n - len(tail)]]))
+    x = np.stack([c - c.astype(np.float64).mean(0, keepdims=True) for c in chunks]).astype(np.float32)
+    with torch.no_grad():
+        _, ref = models_ref.forward(ARCH, torch.from_numpy(x), {k: torch.from_numpy(v) for k, v in sd.items()})
+    ref = ref.numpy().mean(0).astype(np.float64)
+    assert float(e @ ref / np.linalg.norm(e) / np.linalg.norm(ref)) >= 0.9999
+    assert np.abs(e - ref).max() < 1e-4
