@@ -23,9 +23,14 @@ Published algorithm (torchaudio compliance/kaldi.py, v0.12-2.x):
 The reference's own native restatement of the same algorithm is
 runtime/core/frontend/fbank.h:138-198 (+ fft.cc:59-119); it needs glog and is
 therefore not compilable here without a stand-in header, so it is read, not
-built.  **Parity with reference outputs is unpinned** (no fixture holds fbank
-outputs); `fbank()` is cross-checked against `fbank_dft64()` (independent
-float64 direct-DFT formulation) in tests.
+built.  Parity with the reference's own outputs is unpinned (no fixture holds
+fbank outputs, torchaudio is absent); the restatement is **proxy-pinned** to an
+independent third-party implementation of the same algorithm,
+transformers.audio_utils (5.15; the numpy path of its Speech2Text / AST feature
+extractors): the frame pipeline agrees within 5e-6 with the same filters and the
+filters within 2e-5 (float32 rounding) for 23-128 bins, 8 / 16 kHz and every
+window (tests/test_fbank_proxy_cpu.py); `fbank()` is also cross-checked against
+`fbank_dft64()` (independent float64 direct-DFT formulation).
 """
 from __future__ import annotations
 
