@@ -3,6 +3,7 @@ itself is unpinned — kaldiio is absent) and fire-style flag parsing."""
 import struct
 
 import numpy as np
+import pytest
 
 from wespeaker_hubert_amd.bin import _fire
 from wespeaker_hubert_amd.kaldi_io import WriteHelper, load_ark, load_scp_sequential
@@ -104,3 +105,30 @@ def test_load_mat_text(tmp_path):
     p = tmp_path / "t.ark"
     p.write_bytes(b"u1  [\n  1 2.5 -3\n  4 5 6 ]\n")
     np.testing.assert_array_equal(load_mat(f"{p}:4"), np.array([[1, 2.5, -3], [4, 5, 6]], np.float32))
+
+
+def test_load_scp_matrix_equals_sequential_reader(tmp_path):
+    """The vectorised scp reader (scoring CLIs) returns exactly the per-record reader's
+    keys and values: fixed-stride arks (strided view), variable-length keys and several
+    arks in shuffled scp order (gather), and mixed dims / types (fallback)."""
+    from wespeaker_hubert_amd.kaldi_io import load_scp_matrix
+    rng = np.random.default_rng(5)
+    with WriteHelper(f"ark,scp:{tmp_path}/a.ark,{tmp_path}/a.scp") as w:
+        for i in range(40):
+            w(f"u{i:04d}", rng.standard_normal(16).astype(np.float32))
+    with WriteHelper(f"ark,scp:{tmp_path}/b.ark,{tmp_path}/b.scp") as w:
+        for i in range(25):
+            w("k" * (1 + i % 5) + str(i), rng.standard_normal(16).astype(np.float32))
+    with WriteHelper(f"ark,scp:{tmp_path}/c.ark,{tmp_path}/c.scp") as w:
+        w("d0", rng.standard_normal(16))  # float64 (DV)
+        w("f0", rng.standard_normal(8).astype(np.float32))
+    lines = open(tmp_path / "a.scp").read().splitlines() + open(tmp_path / "b.scp").read().splitlines()
+    rng.shuffle(lines)
+    (tmp_path / "m.scp").write_text("\n".join(lines) + "\n\n")
+    for name in ("a.scp", "b.scp", "m.scp"):
+        keys, mat = load_scp_matrix(str(tmp_path / name))
+        ref = list(load_scp_sequential(str(tmp_path / name)))
+        assert keys == [k for k, _ in ref] and mat.dtype == np.float32
+        np.testing.assert_array_equal(mat, np.stack([v for _, v in ref]))
+    with pytest.raises(ValueError):  # mixed dims cannot form one matrix
+        load_scp_matrix(str(tmp_path / "c.scp"))

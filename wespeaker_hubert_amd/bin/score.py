@@ -10,16 +10,16 @@ import sys
 import numpy as np
 import torch
 
-from ..kaldi_io import load_scp_sequential
+from ..kaldi_io import load_scp_matrix
 from ..scoring import group_sums, trials_cosine_score
 from . import _fire
 
 
 def calculate_mean_from_kaldi_vec(scp_path, device="cuda"):
-    embs = [e for _, e in load_scp_sequential(scp_path)]
-    x = torch.from_numpy(np.stack(embs).astype(np.float32)).to(device)
+    _, embs = load_scp_matrix(scp_path)
+    x = torch.from_numpy(np.ascontiguousarray(embs, dtype=np.float32)).to(device)
     acc, cnt = group_sums(x, np.zeros(len(embs), np.int32), 1)
-    return (acc[0] / cnt[0]).cpu().numpy().astype(embs[0].dtype)
+    return (acc[0] / cnt[0]).cpu().numpy().astype(embs.dtype)
 
 
 def main(exp_dir, eval_scp_path, cal_mean, cal_mean_dir, *trials):
@@ -29,7 +29,7 @@ def main(exp_dir, eval_scp_path, cal_mean, cal_mean_dir, *trials):
         scp_path = os.path.join(cal_mean_dir, "xvector.scp")
         mean_vec = calculate_mean_from_kaldi_vec(scp_path)
         np.save(os.path.join(cal_mean_dir, "mean_vec.npy"), mean_vec)
-    emb = dict(load_scp_sequential(eval_scp_path))
+    emb = load_scp_matrix(eval_scp_path)
     store = os.path.join(exp_dir, "scores")
     return trials_cosine_score(emb, trials, store, mean_vec)
 

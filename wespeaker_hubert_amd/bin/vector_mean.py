@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from .. import dist as wdist
-from ..kaldi_io import WriteHelper, load_scp_sequential, validate_path
+from ..kaldi_io import WriteHelper, load_scp_matrix, validate_path
 from ..scoring import group_sums
 
 
@@ -26,18 +26,19 @@ def compute_vector_mean(spk2utt, xvector_scp, spk_xvector_ark, device="cuda"):
             tok = line.strip().split(" ")
             if tok and tok[0]:
                 spk2utts[tok[0]] = tok[1:]
-    utt2emb = dict(load_scp_sequential(xvector_scp))
+    keys, mat = load_scp_matrix(xvector_scp)
+    uidx = {k: i for i, k in enumerate(keys)}
     spks = list(spk2utts.keys())
     rows, groups = [], []
     for gi, spk in enumerate(spks):
         for utt in spk2utts[spk]:
-            rows.append(utt2emb[utt])
+            rows.append(uidx[utt])
             groups.append(gi)
     rank, world = wdist.world()
     lo, hi = wdist.shard_bounds(len(rows), rank, world)
-    dim = rows[0].shape[0]
+    dim = mat.shape[1]
     if hi > lo:
-        x = torch.from_numpy(np.stack(rows[lo:hi]).astype(np.float32)).to(device)
+        x = torch.from_numpy(np.ascontiguousarray(mat[rows[lo:hi]], dtype=np.float32)).to(device)
         acc, cnt = group_sums(x, np.asarray(groups[lo:hi], np.int32), len(spks))
     else:
         acc = torch.zeros(len(spks), dim, dtype=torch.float64, device=device)

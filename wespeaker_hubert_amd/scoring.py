@@ -138,12 +138,23 @@ def read_trials(path: str) -> List[List[str]]:
         return [ln.strip().split() for ln in f if ln.strip()]
 
 
-def trials_cosine_score(emb: Dict[str, np.ndarray], trials: Sequence[str], store_dir: str,
-                        mean_vec: Optional[np.ndarray] = None, device: str = "cuda") -> List[str]:
-    """bin/score.py:38-72 on the GPU; writes `<trial>.score` with `{:.5f}` scores."""
+def as_table(emb) -> Tuple[List[str], np.ndarray, Dict[str, int]]:
+    """Embeddings as (keys, [n][D] float32 matrix, key -> row): a {key: vector} dict or a
+    (keys, matrix) pair from kaldi_io.load_scp_matrix (later duplicates win, as in a dict)."""
+    if isinstance(emb, tuple):
+        keys, mat = emb
+        index = {k: i for i, k in enumerate(keys)}
+        return list(keys), np.ascontiguousarray(mat, dtype=np.float32), index
     keys = list(emb.keys())
-    kidx = {k: i for i, k in enumerate(keys)}
-    E = torch.from_numpy(np.stack([emb[k] for k in keys]).astype(np.float32)).to(device)
+    return keys, np.stack([emb[k] for k in keys]).astype(np.float32), {k: i for i, k in enumerate(keys)}
+
+
+def trials_cosine_score(emb, trials: Sequence[str], store_dir: str,
+                        mean_vec: Optional[np.ndarray] = None, device: str = "cuda") -> List[str]:
+    """bin/score.py:38-72 on the GPU; writes `<trial>.score` with `{:.5f}` scores.  `emb`: a
+    {key: vector} dict or a (keys, matrix) pair (as_table)."""
+    _, mat, kidx = as_table(emb)
+    E = torch.from_numpy(mat).to(device)
     if mean_vec is not None:
         E = E - torch.from_numpy(np.asarray(mean_vec, dtype=np.float32)).to(device)
     out_paths = []
@@ -162,23 +173,23 @@ def trials_cosine_score(emb: Dict[str, np.ndarray], trials: Sequence[str], store
 
 
 def score_norm(score_norm_method: str, top_n: int, trial_score_file: str, score_norm_file: str,
-               cohort: Dict[str, np.ndarray], eval_emb: Dict[str, np.ndarray],
-               mean_vec: Optional[np.ndarray] = None, device: str = "cuda") -> None:
-    """bin/score_norm.py:54-115 (asnorm / snorm) with the statistics on the GPU."""
+               cohort, eval_emb, mean_vec: Optional[np.ndarray] = None, device: str = "cuda") -> None:
+    """bin/score_norm.py:54-115 (asnorm / snorm) with the statistics on the GPU.  `cohort` /
+    `eval_emb`: {key: vector} dicts or (keys, matrix) pairs (as_table)."""
     rows = read_trials(trial_score_file)
     enroll = sorted(set(r[0] for r in rows))
     test = sorted(set(r[1] for r in rows))
-    mv = np.zeros(next(iter(eval_emb.values())).shape, np.float32) if mean_vec is None else \
-        np.asarray(mean_vec, np.float32)
-    ckeys = list(cohort.keys())
-    C = torch.from_numpy(np.stack([cohort[k] for k in ckeys]).astype(np.float32)).to(device)
+    _, emat, eidx = as_table(eval_emb)
+    mv = np.zeros(emat.shape[1], np.float32) if mean_vec is None else np.asarray(mean_vec, np.float32)
+    _, cmat, _ = as_table(cohort)
+    C = torch.from_numpy(cmat).to(device)
     if score_norm_method == "snorm":
         top_n = C.shape[0]
     elif score_norm_method != "asnorm":
         raise ValueError(score_norm_method)
     mvt = torch.from_numpy(mv).to(device)
-    Ee = np.stack([eval_emb[k] for k in enroll]).astype(np.float32)
-    Et = np.stack([eval_emb[k] for k in test]).astype(np.float32)
+    Ee = emat[[eidx[k] for k in enroll]]
+    Et = emat[[eidx[k] for k in test]]
     e_mu, e_sd = asnorm_stats(torch.from_numpy(Ee).to(device), C, top_n, mvt)
     t_mu, t_sd = asnorm_stats(torch.from_numpy(Et).to(device), C, top_n, mvt)
     ei = {k: i for i, k in enumerate(enroll)}
