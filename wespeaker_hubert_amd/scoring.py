@@ -135,7 +135,7 @@ def plot_det_curve(fnr, fpr, save_path: str) -> None:
 # --------------------------------------------------------- file drivers ---
 def read_trials(path: str) -> List[List[str]]:
     with open(path, "r", encoding="utf8") as f:
-        return [ln.strip().split() for ln in f if ln.strip()]
+        return [t for t in (ln.split() for ln in f) if t]
 
 
 def as_table(emb) -> Tuple[List[str], np.ndarray, Dict[str, int]]:
@@ -212,14 +212,11 @@ def score_norm(score_norm_method: str, top_n: int, trial_score_file: str, score_
 
 def compute_metrics(scores_file: str, p_target=0.01, c_miss=1, c_fa=1) -> Tuple[float, float]:
     """bin/compute_metrics.py:25-50 -> (EER %, minDCF)."""
-    scores, labels = [], []
     with open(scores_file) as f:
-        for line in f:
-            tok = line.strip().split()
-            scores.append(float(tok[2]))
-            labels.append(tok[3] == "target")
-    scores = np.hstack(scores)
-    labels = np.hstack(labels)
+        rows = [t for t in (ln.split() for ln in f) if t]
+    # the same float(tok[2]) / tok[3] == "target" per line as the reference, in two list passes
+    scores = np.array([float(t[2]) for t in rows], dtype=np.float64)
+    labels = np.array([t[3] == "target" for t in rows], dtype=bool)
     fnr, fpr = compute_pmiss_pfa_rbst(scores, labels)
     eer, _ = compute_eer(fnr, fpr, scores)
     return 100 * eer, compute_c_norm(fnr, fpr, p_target, c_miss, c_fa)
