@@ -11,7 +11,8 @@
 // (timing only: no split VALU, same LDS / DMA traffic; its outputs differ), 9 = family 7 with the
 // next tile's DMA pieces interleaved into the k-tile's quarters (bit-identical); 10 = family 7's
 // LDS -> split -> MFMA loop alone (no DMA, no barrier in the k-loop; timing only); 11 = 10 without
-// the split (LDS -> MFMA alone; timing only).
+// the split (LDS -> MFMA alone; timing only); 'c' (12) = family 10 (W fragments from L2 into
+// registers, A alone through a 4-deep LDS ring; bit-identical to 6 / 7).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -162,6 +163,7 @@ void run(const Case& c, int v, float* out, double* cs, hipStream_t s) {
   q.out = out;
   q.colsum = cs;
   if (v == 6) x3::t_4x2_2x4_mf16(q, c.whi, c.wlo, s);
+  else if (v == 12) x3::t_gb256(q, c.whi, c.wlo, s);  // family 10 ('c')
   else if (v >= 8) x3::t_g256_xp(q, c.whi, c.wlo, s, v == 8 ? 1 : v == 9 ? 2 : v - 7);  // r6 experiments
   else {
     if (!x3::g256_supported(q)) { std::fprintf(stderr, "%s: family %d does not take these operands\n", c.name.c_str(), v); std::exit(2); }
@@ -201,8 +203,8 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   int bad = 0;
   for (const Case& c : cases) {
-    std::vector<float*> out(12, nullptr);
-    std::vector<double*> cs(12, nullptr);
+    std::vector<float*> out(13, nullptr);
+    std::vector<double*> cs(13, nullptr);
     for (int v : vars) {
       CK(hipMalloc(&out[v], c.out_words * 4));
       CK(hipMemset(out[v], 0xff, c.out_words * 4));

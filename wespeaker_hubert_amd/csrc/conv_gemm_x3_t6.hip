@@ -553,6 +553,210 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
 #undef WSP_GEPI
 }
 
+// ---------------------------------------------------------------------------------------------
+// Tile family 10 (r6): family 7's 256 x 256 tile, waves and epilogue, with W's fragments loaded
+// by each wave straight from L2 into registers (16 B per lane: the [N][Kp] hi / lo images already
+// hold a 16x16x32 B fragment's 8 k of one column contiguously) and only A staged through LDS, in a
+// 4-deep ring of 32 KB stages (family 7: A + W in a 2-deep ring of 64 KB).  Per k-tile a wave
+// reads 8 A fragments from LDS (family 7: 24 fragment reads), issues 4 A DMA pieces (family 7: 8
+// pieces) and 16 B loads, and the barrier that ends k-tile t waits for tile t + 1's A, issued three
+// k-tiles earlier (family 7: one).  Quarters run (0,0) (1,0) (1,1) (0,1) so each B half is dead for
+// half a k-tile before the next tile's copy of it is loaded into the same registers.  Every VMEM
+// op is issued whether or not its tile exists (kOOB offsets past the end: zeros, still counted), so
+// the counted vmcnt waits are exact.  Same products, per-accumulator MFMA order and epilogue as
+// families 6 / 7: bit-identical.
+constexpr int kBStages = 4;
+template <int AM, bool CSK>
+__global__ __launch_bounds__(512, 1) void conv_gemm_gb(const ConvGemmArgs p, const __bf16* __restrict__ whi,
+                                                       const __bf16* __restrict__ wlo) {
+  constexpr bool DENSE = AM == 1;
+  static_assert(AM == 0 || AM == 1, "family 10: uniform k-tiles only");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int ntiles = p.N / 256;
+  const int mtiles = (p.M + 255) / 256;
+  const int wg = xcd_remap(blockIdx.x, ntiles * mtiles);
+  const int mt = wg / ntiles;
+  const int nt = wg - mt * ntiles;
+  const int m0 = mt * 256;
+  const int n0 = nt * 256;
+
+  // ---- A rows of this lane (family 7's mapping)
+  const int ac0 = 4 * ((lane & 7) ^ ((lane >> 4) & 1)), ac1 = ac0 ^ 16;
+  int a_r[4], a_t[DENSE ? 1 : 4], a_l[DENSE ? 1 : 4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + (4 * wave + i) * 8 + (lane >> 3);
+    if constexpr (DENSE) {
+      a_r[i] = m < p.M ? m : -1;
+    } else if (p.seg) {
+      const int mm = m < p.M ? m : p.M - 1;
+      const int b = seg_of(p.seg, p.nseg, mm);
+      const int t = (mm - p.seg[b]) * p.stride;
+      const int* is = p.iseg ? p.iseg : p.seg;
+      a_r[i] = is[b] + t;
+      a_t[i] = (m < p.M) ? t : -0x40000000;
+      a_l[i] = is[b + 1] - is[b];
+    } else {
+      const int b = m / p.T;
+      const int t = (m - b * p.T) * p.stride;
+      a_r[i] = b * p.Ti + t;
+      a_t[i] = (m < p.M) ? t : -0x40000000;
+      a_l[i] = p.Ti;
+    }
+  }
+  const int nk = p.Kp / BK;
+  int jt = 0, ct = 0;  // tap and channel of the next A k-tile to fetch (fetched in order)
+  auto dma_a = [&](int kt) {  // kt >= nk: the same pieces at kOOB (zeros into a stage nobody reads)
+    unsigned char* st = smem + (kt & (kBStages - 1)) * kGA;
+    const bool live = kt < nk;
+    const int off = jt * p.dil - p.pad;
+    const float* base = p.a[0];
+    int ld = p.lda[0], cl = ct;
+    if (ct >= p.cseg[2]) {
+      base = p.a[2];
+      ld = p.lda[2];
+      cl = ct - p.cseg[2];
+    } else if (ct >= p.cseg[1]) {
+      base = p.a[1];
+      ld = p.lda[1];
+      cl = ct - p.cseg[1];
+    }
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(base);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (DENSE) {
+        g_dma(ra, st + (4 * wave + i) * 1024,
+              live && a_r[i] >= 0 ? (a_r[i] * ld + cl + (i & 1 ? ac1 : ac0)) * 4 : kOOB);
+      } else {
+        const int tt = a_t[i] + off;
+        const bool ok = live && tt >= 0 && tt < a_l[i];
+        g_dma(ra, st + (4 * wave + i) * 1024, ok ? ((a_r[i] + off) * ld + cl + (i & 1 ? ac1 : ac0)) * 4 : kOOB);
+      }
+    }
+    ct += 32;
+    if (ct >= p.cin) {
+      ct -= p.cin;
+      ++jt;
+    }
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;  // 4 x 2 waves of 64 x 128
+  const int r16 = lane & 15, qk = lane >> 4;
+  // B fragment (jh, j) of k-tile kt: column n0 + wn 128 + (4 jh + j) 16 + r16, k 32 kt + 8 qk .. + 7
+  const __amdgpu_buffer_rsrc_t rwh = make_rsrc(whi);
+  const __amdgpu_buffer_rsrc_t rwl = make_rsrc(wlo);
+  const int bcol0 = ((n0 + wn * 128 + r16) * p.Kp + 8 * qk) * 2;
+  const int bjstep = 16 * p.Kp * 2;
+  bf16x8 bh[2][4], bl[2][4];
+  auto load_b = [&](int kt, int jh) {
+    const bool live = kt < nk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int o = live ? bcol0 + (4 * jh + j) * bjstep + kt * 64 : kOOB;
+      bh[jh][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rwh, o, 0, 0));
+      bl[jh][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rwl, o, 0, 0));
+    }
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ah[2][2], al[2][2];
+  auto rdA = [&](const unsigned char* st, int ih) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = wm * 64 + (ih * 2 + i) * 16 + r16;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(st + g_aslot(r, 2 * qk));
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(st + g_aslot(r, 2 * qk + 1));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const __bf16 h0 = (__bf16)x0[e], h1 = (__bf16)x1[e];
+        ah[ih][i][e] = h0;
+        ah[ih][i][4 + e] = h1;
+        al[ih][i][e] = (__bf16)(x0[e] - (float)h0);
+        al[ih][i][4 + e] = (__bf16)(x1[e] - (float)h1);
+      }
+    }
+  };
+  auto mm = [&](int ih, int jh) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f32x4& c = acc[ih * 2 + i][jh * 4 + j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[ih][i], bh[jh][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ih][i], bl[jh][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ih][i], bh[jh][j], c, 0, 0, 0);
+      }
+  };
+
+  // prologue: A tiles 0..3 and both B halves of tile 0, all waited for
+  dma_a(0);
+  dma_a(1);
+  dma_a(2);
+  dma_a(3);
+  load_b(0, 0);
+  load_b(0, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // Per k-tile t, VMEM issue order: B half 0 of t + 1 (8), B half 1 of t + 1 (8), and after the
+  // barrier A of t + 4 (4).  Waits: B half 0 of t has B half 1 of t and A of t + 3 behind it (12);
+  // B half 1 of t has A of t + 3 and B half 0 of t + 1 behind it (12); A of t + 1 (issued after
+  // the barrier of t - 3) has 3 x 16 B loads and 2 x 4 A pieces behind it at the barrier of t (56).
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* st = smem + (kt & (kBStages - 1)) * kGA;
+    // (the B registers' loads are register dependencies: hipcc places their vmcnt waits itself;
+    // only the LDS-DMA data below needs a counted wait)
+    rdA(st, 0);
+    mm(0, 0);
+    rdA(st, 1);  // its reads and split interleave with quarter (0,0)'s MFMAs
+    mm(1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    load_b(kt + 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(1, 1);
+    mm(0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    load_b(kt + 1, 1);
+    // A of kt + 1 has landed and every wave is done reading this stage
+    asm volatile("s_waitcnt vmcnt(56) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    dma_a(kt + 4);
+  }
+  // every DMA (including the zero pieces past the end) has landed and every wave is past its
+  // last LDS read before the epilogue reuses LDS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#define WSP_GBEPI(RB, RES)                                                                                  \
+  switch (p.act) {                                                                                         \
+    case kActRelu: g_epilogue_rows<kActRelu, RB, RES>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;    \
+    case kActTanh: g_epilogue_rows<kActTanh, RB, RES>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;    \
+    case kActGelu: g_epilogue_rows<kActGelu, RB, RES>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;    \
+    default: g_epilogue_rows<kActNone, RB, RES>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;          \
+  }
+  if constexpr (CSK) {
+    switch (p.act) {
+      case kActRelu: g_epilogue_cs<kActRelu>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;
+      case kActTanh: g_epilogue_cs<kActTanh>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;
+      case kActGelu: g_epilogue_cs<kActGelu>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;
+      default: g_epilogue_cs<kActNone>(p, acc, m0, n0, wm, wn, wave, lane, smem); break;
+    }
+  } else if (p.res) {
+    WSP_GBEPI(false, true)
+  } else if (p.row_bias) {
+    WSP_GBEPI(true, false)
+  } else {
+    WSP_GBEPI(false, false)
+  }
+#undef WSP_GBEPI
+}
+
 }  // namespace
 
 namespace x3 {
@@ -602,6 +806,28 @@ void t_g256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t
     hipLaunchKernelGGL((conv_gemm_g<0, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
   else
     hipLaunchKernelGGL((conv_gemm_g<2, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
+  WSP_HIP(hipGetLastError());
+}
+
+// family 10: the operands family 7 takes on uniform k-tiles (no LayerNorm fold)
+bool gb256_supported(const ConvGemmArgs& p) {
+  return g256_supported(p) && uniform_ktiles(p) && !p.lnmode && p.Kp % BK == 0;
+}
+
+void t_gb256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s) {
+  WSP_CHECK(gb256_supported(p), "conv_gemm_x3 family 10: unsupported operands");
+  const int nwg = ((p.M + 255) / 256) * (p.N / 256);
+  constexpr int lds0 = kBStages * kGA > kGEpiBytes ? kBStages * kGA : kGEpiBytes;
+  constexpr int lds = lds0 > kGCsBytes ? lds0 : kGCsBytes;
+  const bool dense = p.taps == 1 && p.pad == 0 && p.stride == 1 && !p.iseg && (p.seg || p.Ti == p.T);
+  if (p.colsum && dense)
+    hipLaunchKernelGGL((conv_gemm_gb<1, true>), dim3(nwg), dim3(512), lds, s, p, h, l);
+  else if (p.colsum)
+    hipLaunchKernelGGL((conv_gemm_gb<0, true>), dim3(nwg), dim3(512), lds, s, p, h, l);
+  else if (dense)
+    hipLaunchKernelGGL((conv_gemm_gb<1, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
+  else
+    hipLaunchKernelGGL((conv_gemm_gb<0, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
   WSP_HIP(hipGetLastError());
 }
 
