@@ -362,8 +362,6 @@ void t_4x2_2x4_sw1(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_
 void t_4x2_2x4_mf16(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);  // v5 on 16x16x32 (v6)
 bool g256_supported(const ConvGemmArgs&);                                              // v7 operands
 void t_g256(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);         // v6 by LDS-DMA (v7)
-bool gb256_supported(const ConvGemmArgs&);                                             // v10 operands
-void t_gb256(const ConvGemmArgs&, const __bf16*, const __bf16*, hipStream_t);        // v7, W from L2 (v10)
 }  // namespace x3
 
 }  // namespace wsp

@@ -553,6 +553,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
 #undef WSP_GEPI
 }
 
+#ifdef WSP_G7_XP
 // ---------------------------------------------------------------------------------------------
 // Tile family 10 (r6): family 7's 256 x 256 tile, waves and epilogue, with W's fragments loaded
 // by each wave straight from L2 into registers (16 B per lane: the [N][Kp] hi / lo images already
@@ -564,7 +565,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
 // half a k-tile before the next tile's copy of it is loaded into the same registers.  Every VMEM
 // op is issued whether or not its tile exists (kOOB offsets past the end: zeros, still counted), so
 // the counted vmcnt waits are exact.  Same products, per-accumulator MFMA order and epilogue as
-// families 6 / 7: bit-identical.
+// families 6 / 7: bit-identical — and 1.5-1.7x slower (profiles/r6d_gemm_family10.txt): the four
+// waves of a column half each fetch the same W fragments, so a 64-k tile moves 160 KB through the
+// CU's vector-memory address path (family 7: 128 KB per two 32-k tiles, each byte once), which at
+// ~64 B/clk outlasts the tile's MFMA issue.  Development build only (tools/gemm_check, WSP_G7_XP).
 constexpr int kBStages = 4;
 template <int AM, bool CSK>
 __global__ __launch_bounds__(512, 1) void conv_gemm_gb(const ConvGemmArgs p, const __bf16* __restrict__ whi,
@@ -756,6 +760,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_gb(const ConvGemmArgs p, con
   }
 #undef WSP_GBEPI
 }
+#endif  // WSP_G7_XP
 
 }  // namespace
 
@@ -809,7 +814,8 @@ void t_g256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t
   WSP_HIP(hipGetLastError());
 }
 
-// family 10: the operands family 7 takes on uniform k-tiles (no LayerNorm fold)
+#ifdef WSP_G7_XP
+// family 10 (development build): the operands family 7 takes on uniform k-tiles (no LayerNorm fold)
 bool gb256_supported(const ConvGemmArgs& p) {
   return g256_supported(p) && uniform_ktiles(p) && !p.lnmode && p.Kp % BK == 0;
 }
@@ -831,7 +837,6 @@ void t_gb256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_
   WSP_HIP(hipGetLastError());
 }
 
-#ifdef WSP_G7_XP
 // development entry (tools/gemm_check): plain family 7 operand forms (no LayerNorm fold)
 void t_g256_xp(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s, int xp) {
   const int nwg = ((p.M + 255) / 256) * (p.N / 256);
