@@ -75,8 +75,9 @@ __device__ __forceinline__ void stage_patch(__amdgpu_buffer_rsrc_t rx, int F, in
     const int c = (q - ir * G::C4) * 4;
     const int pf = ir / PT;
     const int f = f0 - 1 + pf, t = t0 - 1 + (ir - pf * PT);
-    const bool ok = q < G::IR * G::C4 && f >= 0 && f < F && t >= 0 && t < T;
-    v[i] = bload4(rx, ok ? ((f * T + t) * C + c) * 4 : kOOB);
+    // unsigned range tests joined by & (not &&): compare + select, no exec-mask branches
+    const bool ok = (q < G::IR * G::C4) & ((unsigned)f < (unsigned)F) & ((unsigned)t < (unsigned)T);
+    v[i] = bload4(rx, ok ? (int)((((unsigned)f * T + t) * C + c) * 4) : kOOB);
   }
 #pragma unroll
   for (int i = 0; i < G::NQ; ++i) {
@@ -578,9 +579,15 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res + obase);
   const int tw = t0 + 4 * h;  // time of register 0
   const int fw = f0 + RW * pp;  // frequency row of the wave's first run
-  auto roff = [&](int i, int col, int r) {
-    const int t = tw + (r & 3) + 8 * (r >> 2);
-    return fw + i < p.F && t < p.T ? (((fw + i) * p.T + t) * C4 + col) * 4 : kOOB;
+  // register r holds time tw + tro(r): inside the utterance iff tro(r) < T - tw.  Run i's limit
+  // folds its frequency-row test (and a dead load's) into that one compare, so every offset is a
+  // compare + select: the nested conditional form compiled to exec-mask branches (and predicate
+  // spills to VGPR lanes) around each of the 32 residual loads inside conv1's MFMA stream
+  auto tro = [](int r) { return (r & 3) + 8 * (r >> 2); };
+  auto rlim = [&](int i, bool live) { return live && fw + i < p.F ? p.T - tw : 0; };
+  auto roff = [&](int i, int col, int r, int lim) {
+    const unsigned o = (((unsigned)(fw + i) * p.T + tw + tro(r)) * C4 + col) * 4;
+    return tro(r) < lim ? (int)o : kOOB;
   };
   float rv[RW][16], b3v;
   const __amdgpu_buffer_rsrc_t rb3 = make_rsrc(p.b3);
@@ -588,11 +595,12 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
     const int col = (GW * c + g) * 32 + r32;
     b3v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb3, live ? col * 4 : kOOB, 0, 0));
 #pragma unroll
-    for (int i = 0; i < RW; ++i)
+    for (int i = 0; i < RW; ++i) {
+      const int lim = rlim(i, live);
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        rv[i][r] = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(rr, live ? roff(i, col, r) : kOOB, 0, 0));
+        rv[i][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, roff(i, col, r, lim), 0, 0));
+    }
   };
 
   // ---- phase 1: conv2 for the wave's two runs, channel tile g; transposed accumulators
@@ -765,7 +773,9 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
       else w3load(c + 1, q + RD3 - KS3, ch_[q % RD3], cl_[q % RD3]);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (c == 1) WSP_TAIL_STAMP(8);
     if (c > 0) sync();  // every wave is done reading chunk c - 1 from the buffer
+    if (c == 1) WSP_TAIL_STAMP(9);
     // epilogue: out = relu(a3 + b3 + res) -> HBM and as bf16 hi / lo rows of the chunk buffer.
     // The first wait covering these stores is the one on the W1 fetch that conv1's k-step 0
     // issues after them, RD1 k-steps later (stores count in vmcnt like loads)
@@ -773,10 +783,11 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
       const int col = (GW * c + g) * 32 + r32;
 #pragma unroll
       for (int i = 0; i < RW; ++i) {
+        const int lim = rlim(i, true);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float y = fmaxf(a3[i][r] + b3v + rv[i][r], 0.f);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, roff(i, col, r), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, roff(i, col, r, lim), 0, 0);
           // lanes l, l ^ 1 hold columns c, c ^ 1: the even lane stores both hi halves, the odd
           // lane both lo halves
           const __bf16 hh = (__bf16)y;
@@ -795,7 +806,9 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
         }
       }
     }
+    if (c == 1) WSP_TAIL_STAMP(10);
     sync();  // the chunk's GW x 32 channels of every run are in LDS
+    if (c == 1) WSP_TAIL_STAMP(11);
     // next conv1: k-steps KB c .. KB c + KB - 1, output tile g, the wave's two runs
     read_cb(0, ah[0], al[0]);
 #pragma unroll
@@ -815,15 +828,15 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
     const int col = g * 32 + r32;
     const float bv = p.b1n[col];
 #pragma unroll
-    for (int i = 0; i < RW; ++i)
+    for (int i = 0; i < RW; ++i) {
+      const int lim = rlim(i, true);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int t = tw + (r & 3) + 8 * (r >> 2);
         const float y = fmaxf(acc1[i][r] + bv, 0.f);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ry,
-                                              fw + i < p.F && t < p.T ? (((fw + i) * p.T + t) * C + col) * 4 : kOOB,
-                                              0, 0);
+        const unsigned o = (((unsigned)(fw + i) * p.T + tw + tro(r)) * C + col) * 4;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ry, tro(r) < lim ? (int)o : kOOB, 0, 0);
       }
+    }
   }
   WSP_TAIL_STAMP(15);
 }
