@@ -487,11 +487,18 @@ __global__ __launch_bounds__(256, 2) void res2_strip_kernel(const Res2Args p) {
             const int m0 = abase + i * 32 + 4 * h;  // row of register 0
             const int lo = -m0, hi = M - m0;
             const int b0 = (m0 * p.ldx + acol + col) * 4;
+            if (abase + i * 32 >= 0 && abase + i * 32 + 32 <= M) {  // wave-uniform: every row in range
   #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int rr = (r & 3) + 8 * (r >> 2);
-              nx[i][r] = __builtin_bit_cast(
-                  float, __builtin_amdgcn_raw_buffer_load_b32(rx, (rr >= lo && rr < hi) ? b0 + rr * ldx4 : kOOB, 0, 0));
+              for (int r = 0; r < 16; ++r)  // row step in the scalar offset: no per-register VALU
+                nx[i][r] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rx, b0, ((r & 3) + 8 * (r >> 2)) * ldx4, 0));
+            } else {
+  #pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const int rr = (r & 3) + 8 * (r >> 2);
+                nx[i][r] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rx, (rr >= lo && rr < hi) ? b0 + rr * ldx4 : kOOB, 0, 0));
+              }
             }
           }
           if (step == 6 && tid < 2 * d * (W / 4)) {  // the next chunk's X_0 history rows
@@ -511,6 +518,16 @@ __global__ __launch_bounds__(256, 2) void res2_strip_kernel(const Res2Args p) {
         // next chunk's X_0) -> image rows [2d, 2d + kSR); X_step's last 2d rows -> history
         const int cp = col & ~1;
         unsigned char* hslot = hist + (step - 1) * (kSHistRows * 2 * kSRB);  // X_step's slot (step >= 1)
+        // image byte offsets (within a plane; the lo plane is kSPlane above the hi one): tile 0's
+        // registers 0..3 are image rows ib .. ib + 3; register r + 4 is 8 rows down, which flips bit
+        // 3 of the row's XOR swizzle ((a ^ 128) + 8 rows); r + 8 and tile i + 1 are 16 and 32 rows
+        // down, same swizzle — 4 computed offsets per lane and conv instead of one per register
+        const bool odd = lane & 1;
+        const int ib = 2 * dq + 4 * h;
+        int a4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a4[k] = (ib + k) * kSRB + s_off(ib + k, cp);
+        unsigned char* img = xhi + (odd ? kSPlane : 0);
         // MODE 0: stores only (the strip's last conv 6); 1: X_{step+1} = sp + spx[step+1];
         // 2: the next chunk's X_0 = spx[0].  FULL: every row of the chunk is owned (no
         // per-row bounds).  Uniform choices hoisted out of the 48-register loop.
@@ -527,24 +544,27 @@ __global__ __launch_bounds__(256, 2) void res2_strip_kernel(const Res2Args p) {
             for (int r = 0; r < 16; ++r) {
               const int rr = (r & 3) + 8 * (r >> 2);
               const float y = fmaxf(acc[i][r] + bv, 0.f) * sc + sh;
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rout,
-                                                    (FULL || (rr >= olo && rr < ohi)) ? b0 + rr * ldo4 : kOOB, 0, 0);
+              if constexpr (FULL)  // every row owned: the row step rides in the scalar offset
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rout, b0, rr * ldo4, 0);
+              else
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), rout,
+                                                      rr >= olo && rr < ohi ? b0 + rr * ldo4 : kOOB, 0, 0);
               if constexpr (MODE != 0) {
                 const float x = MODE == 1 ? y + nx[i][r] : nx[i][r];
                 const __bf16 hh = (__bf16)x;
                 const __bf16 ll = (__bf16)(x - (float)hh);
                 // lanes l, l^1 hold channels col, col^1 of this row: the even lane writes
                 // both hi halves, the odd lane both lo halves (one 4-B store each)
-                const unsigned send = (lane & 1) ? bf_bits(hh) : bf_bits(ll);
+                const unsigned send = odd ? bf_bits(hh) : bf_bits(ll);
                 const unsigned recv = (unsigned)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
-                const int ir = 2 * dq + lr0 + rr;
-                const int o = s_off(ir, cp);
-                unsigned char* img = (lane & 1) ? xlo : xhi;
-                unsigned* dst = reinterpret_cast<unsigned*>(img + ir * kSRB + o);
+                const int ir = ib + 32 * i + rr;
+                const int a = ((r >> 2) & 1 ? (a4[r & 3] ^ 128) + 8 * kSRB : a4[r & 3]) + ((r >> 3) * 16 + 32 * i) * kSRB;
+                unsigned* dst = reinterpret_cast<unsigned*>(img + a);
                 if (NA == TM && i == TM - 1 && ir >= kSR) {  // X_step's rows [kSR, kSR + 2d): save before overwriting
-                  if (step >= 1) *reinterpret_cast<unsigned*>(hslot + ((ir - kSR) * 2 + (lane & 1)) * kSRB + o) = *dst;
+                  if (step >= 1)
+                    *reinterpret_cast<unsigned*>(hslot + ((ir - kSR) * 2 + (lane & 1)) * kSRB + (a - ir * kSRB)) = *dst;
                 }
-                *dst = (lane & 1) ? (recv | ((unsigned)bf_bits(ll) << 16)) : ((unsigned)bf_bits(hh) | (recv << 16));
+                *dst = odd ? (recv | ((unsigned)bf_bits(ll) << 16)) : ((unsigned)bf_bits(hh) | (recv << 16));
               }
             }
           }
