@@ -599,20 +599,7 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
       const int lim = rlim(i, live);
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-#if defined(WSP_TAIL_XP_NORES)  // timing experiments (tools/tail_check built with them): no residual loads
-        rv[i][r] = (float)(lim + r);
-#elif defined(WSP_TAIL_XP_RES128)  // the same bytes in 16-B pieces: lane = position, 4 channels per load
-      {
-        if ((r & 3) == 0) {
-          const int pos = t0 + r32, ch = (GW * c + g) * 32 + 8 * (r >> 2) + 4 * h;
-          const unsigned o = (((unsigned)(fw + i) * p.T + pos) * C4 + ch) * 4;
-          const f32x4 v = bload4(rr, r32 < lim + 4 * h ? (int)o : kOOB);
-          rv[i][r] = v[0]; rv[i][r + 1] = v[1]; rv[i][r + 2] = v[2]; rv[i][r + 3] = v[3];
-        }
-      }
-#else
         rv[i][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, roff(i, col, r, lim), 0, 0));
-#endif
     }
   };
 
@@ -803,21 +790,7 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float y = fmaxf(a3[i][r] + b3v + rv[i][r], 0.f);
-#if defined(WSP_TAIL_XP_OUT128)  // timing experiment: the same bytes in 16-B pieces (lane = position)
-          {
-            typedef unsigned xu4 __attribute__((ext_vector_type(4)));
-            float* yq = &rv[i][r & ~3];  // rv[i] is dead past this element: park y there
-            yq[r & 3] = y;
-            if ((r & 3) == 3) {
-              const int pos = t0 + r32, ch = (GW * c + g) * 32 + 8 * (r >> 2) + 4 * h;
-              const unsigned o = (((unsigned)(fw + i) * p.T + pos) * C4 + ch) * 4;
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(xu4, f32x4{yq[0], yq[1], yq[2], yq[3]}), ro,
-                                                     r32 < lim + 4 * h ? (int)o : kOOB, 0, 0);
-            }
-          }
-#elif !defined(WSP_TAIL_XP_NOSTORE)  // timing experiment (tools/tail_check built with it): no block output
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, roff(i, col, r, lim), 0, 0);
-#endif
           // lanes l, l ^ 1 hold columns c, c ^ 1: the even lane stores both hi halves, the odd
           // lane both lo halves — one 4-B store per lane at a lane-parity plane offset, the word
           // assembled by shifts (an if / else on the parity compiled to two half-masked stores
