@@ -62,7 +62,10 @@ void Model::create(const std::string& arch, int feat_dim, int embed_dim, bool em
     // ceil(feat_dim / 8): the reference model only runs for multiples of 8
     WSP_CHECK(feat_dim >= 8 && feat_dim % 8 == 0, "ResNet feat_dim must be a positive multiple of 8");
     m.ecapa = false;
-    m.x3_variant = 4;  // 256 x 128 swizzled: with the residual prefetch (ROLE 2) +1.3 % C3 over variant 3 (r2c)
+    // basic blocks: 256 x 128 swizzled (with the residual prefetch, ROLE 2: +1.3 % C3 over variant 3,
+    // r2c); bottleneck ResNets: family 7 wherever it takes the operands (1x1 convs with N % 256 == 0),
+    // family 6 elsewhere — ResNet293 C3 +0.2-0.4 % over 4 in three interleaved pairs (r6u)
+    m.x3_variant = it->second.first ? 7 : 4;
     m.streams = 2;     // two utterance ranges in flight: ResNet293 C3 +8.6 %
     m.bottleneck = it->second.first;
     for (int i = 0; i < 4; ++i) m.nblocks[i] = it->second.second[i];
