@@ -115,6 +115,28 @@ def test_resnet_matches_oracle(arch, B, T):
     _assert_emb(emb.cpu().numpy(), ref.numpy())
 
 
+@pytest.mark.parametrize("arch,B,T,res_tail", [("ResNet50", 2, 131, 1), ("ResNet101", 3, 57, 0)])
+def test_resnet_fused_conv3_shortcut(arch, B, T, res_tail):
+    """Bottleneck conv3 + projection shortcut as one GEMM over [y2 | strided x] (option sc_fuse,
+    tile family 7 AM 3): against the oracle, and against the two-GEMM form (sc_fuse 0) within
+    the summation-order difference; res_tail 0 puts every stage's first block (stride 2 and the
+    stride-1 channel change) on the fused path."""
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    m = HipSpeakerModel(arch, feat_dim=80, embed_dim=256)
+    sd = synth_state_dict(29, m.state_dict_layout(), residual_tame=True)
+    m.load_state_dict(sd)
+    m.to(DEV)
+    m.set_option("res_tail", res_tail)
+    x = torch.from_numpy(synth_feats(97, B, T, 80)).to(DEV)
+    _, fused = m(x)
+    m.set_option("sc_fuse", 0)
+    _, split = m(x)
+    with torch.no_grad():
+        _, ref = models_ref.forward(arch, x.cpu(), {k: torch.from_numpy(v) for k, v in sd.items()})
+    _assert_emb(fused.cpu().numpy(), ref.numpy())
+    assert float((fused - split).abs().max()) <= 1e-5 * max(1.0, float(split.abs().max()))
+
+
 @pytest.mark.parametrize("feat_dim", [136, 72])
 def test_resnet_split_k_head_partial_slice(feat_dim):
     """The TSTP head's split-K linear (ops.hip small_linear_splitk_kernel, K >= 4096): feat_dim 136

@@ -68,6 +68,8 @@ void launch_conv_gemm_x3(const ConvGemmArgs& args, const void* whi, const void* 
   x3::TileFn f;
   WSP_CHECK(!p.lnmode || (variant == 7 && x3::g256_supported(p)),
             "conv_gemm_x3: the LayerNorm fold runs on tile family 7 only");
+  WSP_CHECK(!p.sc2d || (variant == 7 && x3::g256_supported(p)),
+            "conv_gemm_x3: conv3 + shortcut runs on tile family 7 only (N % 256 == 0, 16-B aligned operands)");
   if (variant == 7 && x3::g256_supported(p)) {
     // variant 7 (r4): the 256 x 256 16x16x32 tile with every operand staged by LDS-DMA and the
     // fp32 A split at fragment time (conv_gemm_x3_t6.hip); bit-identical to 6, which serves

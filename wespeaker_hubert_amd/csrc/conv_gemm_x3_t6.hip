@@ -317,7 +317,8 @@ template <int AM, bool CSK, int LNM = 0, int XP = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, const __bf16* __restrict__ whi,
                                                       const __bf16* __restrict__ wlo) {
   using L = Lds<true, 16>;
-  constexpr bool DENSE = AM == 1;
+  // AM 3: AM 1 whose A segment 1 is the projection shortcut's 2-D strided input (ConvGemmArgs::sc2d)
+  constexpr bool DENSE = AM == 1 || AM == 3;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -334,12 +335,17 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
   // l row + (l >> 3), slot l & 7 <- source chunk (l & 7) ^ swizzle(row) (ALoader's row logic)
   // row = 32 w + 8 i + (l >> 3): swizzle(row) = (row >> 1) & 5 = ((l >> 4) & 1) | ((i & 1) << 2)
   const int ac0 = 4 * ((lane & 7) ^ ((lane >> 4) & 1)), ac1 = ac0 ^ 16;
-  int a_r[4], a_t[DENSE ? 1 : 4], a_l[DENSE ? 1 : 4];
+  int a_r[4], a_t[DENSE ? 1 : 4], a_l[DENSE ? 1 : 4], a_s[AM == 3 ? 4 : 1];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + (4 * wave + i) * 8 + (lane >> 3);
     if constexpr (DENSE) {
       a_r[i] = m < p.M ? m : -1;
+      if constexpr (AM == 3) {  // shortcut input row of output (b, fo, to)
+        const int fto = p.Fo * p.To;
+        const int b = m / fto, fo = (m - b * fto) / p.To, to = m - b * fto - fo * p.To;
+        a_s[i] = m < p.M ? (b * p.Fi + fo * p.stride) * p.Ti + to * p.stride : -1;
+      }
     } else if (p.seg) {
       const int mm = m < p.M ? m : p.M - 1;
       const int b = seg_of(p.seg, p.nseg, mm);
@@ -387,7 +393,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_g(const ConvGemmArgs p, cons
     for (int i = 0; i < 4; ++i) {
       if (!(part & 1)) break;
       if constexpr (DENSE) {
-        g_dma(ra, st + (4 * wave + i) * 1024, a_r[i] >= 0 ? (a_r[i] * ld + cl + (i & 1 ? ac1 : ac0)) * 4 : kOOB);
+        const int ar = AM == 3 && ct >= p.cseg[1] ? a_s[i] : a_r[i];
+        g_dma(ra, st + (4 * wave + i) * 1024, ar >= 0 ? (ar * ld + cl + (i & 1 ? ac1 : ac0)) * 4 : kOOB);
       } else if constexpr (AM == 2) {
         const int k = kt * BK + (i & 1 ? ac1 : ac0);
         const int tap = k / p.cin;
@@ -772,7 +779,8 @@ bool g256_supported(const ConvGemmArgs& p) {
                        a16(p.row_bias) && a16(p.res) && (!p.res || p.ldres % 4 == 0);
   // non-uniform k-tiles (AM 2): one A segment only, as ALoader's per-lane path
   return aligned && p.N % 256 == 0 && !p.conv2d && !p.gcols && p.amode == kACat &&
-         (uniform_ktiles(p) || (p.cseg[1] >= p.cin && !p.colsum));
+         (uniform_ktiles(p) || (p.cseg[1] >= p.cin && !p.colsum)) &&
+         (!p.sc2d || (uniform_ktiles(p) && !p.colsum && !p.lnmode && !p.row_bias));
 }
 
 void t_g256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t s) {
@@ -783,6 +791,11 @@ void t_g256(const ConvGemmArgs& p, const __bf16* h, const __bf16* l, hipStream_t
   // input offsets, and uniform batches with Ti == T); ragged iseg / Ti != T 1x1 GEMMs take AM 0.
   const bool dense = p.taps == 1 && p.pad == 0 && p.stride == 1 && !p.iseg && (p.seg || p.Ti == p.T);
   const int am = !uniform_ktiles(p) ? 2 : dense ? 1 : 0;
+  if (p.sc2d) {  // conv3 + projection shortcut (check_conv_args / g256_supported: dense, uniform k-tiles)
+    hipLaunchKernelGGL((conv_gemm_g<3, false>), dim3(nwg), dim3(512), lds, s, p, h, l);
+    WSP_HIP(hipGetLastError());
+    return;
+  }
   if (p.lnmode) {
     // LayerNorm fold: 1 = emit (out_proj / fc2 on the residual), 2 = fold (qkv / fc1), 4 = residual
     // normalised on the fly, 5 = both (fc2 / out_proj under the full fold)

@@ -564,7 +564,7 @@ inline void check_conv_args(const ConvGemmArgs& p, const char* who) {
   const std::string w(who);
   // buffer-load byte offsets are 32-bit: every operand must stay below 2 GiB
   // input rows: 1-D strided convs read (M / T) * Ti rows; 2-D reads B*Fi*Ti
-  const long long in_rows = p.conv2d ? (long long)(p.M / (p.Fo * p.To)) * p.Fi * p.Ti
+  const long long in_rows = (p.conv2d || p.sc2d) ? std::max<long long>(p.M, (long long)(p.M / (p.Fo * p.To)) * p.Fi * p.Ti)
                             : p.seg ? (long long)std::max(p.M, p.Ti)
                                      : std::max<long long>(p.M, (long long)((p.M + p.T - 1) / p.T) * p.Ti);
   for (int i = 0; i < 3; ++i)
@@ -584,6 +584,11 @@ inline void check_conv_args(const ConvGemmArgs& p, const char* who) {
     WSP_CHECK(p.taps % p.kw == 0 && p.stride >= 1, w + ": bad 2-D taps/stride");
   }
   for (int i = 0; i < 3; ++i) WSP_CHECK(p.lda[i] % 4 == 0, w + ": lda must be a multiple of 4");
+  if (p.sc2d)
+    WSP_CHECK(!p.conv2d && !p.seg && p.taps == 1 && p.pad == 0 && p.amode == kACat && p.cseg[1] % 32 == 0 &&
+                  p.cseg[2] == p.cin && p.stride >= 1 && p.Fo >= 1 && p.To >= 1 && p.M % (p.Fo * p.To) == 0 &&
+                  (p.Fo - 1) * p.stride < p.Fi && (p.To - 1) * p.stride < p.Ti,
+              w + ": conv3 + shortcut needs a dense 1x1 segment and a 2-D strided segment");
   if (!p.conv2d) WSP_CHECK(p.stride >= 1 && p.Ti >= 1, w + ": call normalized() first");
   if (p.seg) WSP_CHECK(!p.conv2d && p.nseg >= 1 && (p.iseg || p.stride == 1), w + ": segmented batch needs a 1-D conv (input offsets when strided)");
   WSP_CHECK(!p.res || (!p.row_bias && !p.colsum), w + ": a residual epilogue has no row bias / column sums");

@@ -46,6 +46,12 @@ struct ConvGemmArgs {
   // taps = kh*kw with tap j = kf*kw + kt, input (fo*stride + kf - pad, to*stride + kt - pad).
   int conv2d;
   int Fi, Ti, Fo, To, stride, kw;
+  // ResNet bottleneck conv3 + projection shortcut in one 1x1 GEMM (x3 tile family 7 only): A
+  // segment 0 (channels [0, cseg[1])) is dense, row m; segment 1 ([cseg[1], cseg[2])) is read at
+  // the shortcut's 2-D strided position of output row m = (b*Fo + fo)*To + to, input row
+  // (b*Fi + fo*stride)*Ti + to*stride of a[1] (conv2d stays 0; Fi / Ti / Fo / To / stride carry
+  // the shortcut geometry).
+  int sc2d;
   // 1-D strided conv (HuBERT feature extractor): rows m = b*T + t read input
   // frame t*stride + j*dil - pad of [b][Ti]; stride 0 -> 1, Ti 0 -> T.
   // Grouped conv (HuBERT pos_conv): output columns are grouped gcols wide
@@ -82,7 +88,7 @@ struct ConvGemmArgs {
 
 // Fills the 1-D defaults (stride 1, Ti = T) of a zero-initialised ConvGemmArgs.
 inline ConvGemmArgs normalized(ConvGemmArgs p) {
-  if (!p.conv2d) {
+  if (!p.conv2d && !p.sc2d) {
     if (p.stride <= 0) p.stride = 1;
     if (p.Ti <= 0) p.Ti = p.T;
   }

@@ -240,6 +240,9 @@ void Model::set_option(const std::string& key, int value) {
   } else if (key == "res_prefetch") {
     WSP_CHECK(value == 0 || value == 1, "res_prefetch must be 0 or 1");
     impl->res_prefetch = value;
+  } else if (key == "sc_fuse") {
+    WSP_CHECK(value == 0 || value == 1, "sc_fuse must be 0 or 1");
+    impl->sc_fuse = value;
   } else if (key == "res_tail") {
     WSP_CHECK(value >= 0 && value <= 2, "res_tail must be 0 (off), 1 (tail + next conv1) or 2 (tail alone)");
     impl->res_tail = value;
@@ -298,6 +301,7 @@ int Model::get_option(const std::string& key) const {
   if (key == "cat_gate") return m.cat_gate;
   if (key == "res_prefetch") return m.res_prefetch;
   if (key == "res_tail") return m.res_tail;
+  if (key == "sc_fuse") return m.sc_fuse;
   if (key == "astp_fused") return m.astp_fused_on;
   if (key == "attn_pipe") return m.attn_pipe;
   if (key == "pos_conv") return m.pos_conv;

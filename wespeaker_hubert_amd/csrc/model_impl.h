@@ -156,6 +156,7 @@ struct Model::Impl {
   // next block's conv1 on the tail's output while it is on chip (tail2_kernel: two position runs
   // per wave), 2 = the tail alone, 0 = off
   int res_tail = 1;
+  int sc_fuse = 1;  // bottleneck conv3 + projection shortcut as one GEMM (RBlock::c3sc)
   bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
   int res2_variant = 4;  // res2_chain.hip kernel variant (option "res2_variant"; 4 = halo-free strips, C2 1.48 -> 1.24 ms/step; c512 widths run 3)
   ConvW conv, pool1, pool2;
@@ -179,6 +180,10 @@ struct Model::Impl {
   float* stem_b = nullptr;
   struct RBlock {
     ConvW c1, c2, c3, sc;
+    // conv3 (bn3 folded) and the projection shortcut (its bn folded) as ONE 1x1 GEMM over
+    // [y2 | strided x] (K = planes + in_planes, bias b3 + b_sc): the shortcut's output never goes
+    // through HBM (option "sc_fuse"; bottleneck blocks off the fused-tail path, N % 256 == 0)
+    ConvW c3sc;
     void* w3acc = nullptr;  // conv3 (bn3 folded) as pack_frag_acc B fragments for bottleneck_tail
     void* w1frag = nullptr;  // conv1 (bn1 folded) as pack_frag B fragments: run inside the previous block's tail
     bool has_sc = false;
@@ -542,6 +547,22 @@ struct Model::Impl {
           rb.c2 = pack_conv_bn(p + ".conv2.weight", p + ".bn2", rb.planes, rb.planes, 9);
         }
         if (rb.has_sc) rb.sc = pack_conv_bn(p + ".shortcut.0.weight", p + ".shortcut.1", rb.out_planes, rb.in_planes, 1);
+        if (bottleneck && rb.has_sc && rb.out_planes % 256 == 0 && rb.planes % 32 == 0 && rb.in_planes % 32 == 0) {
+          std::vector<double> s3, h3, ss, hs;
+          bn_affine(p + ".bn3", s3, h3);
+          bn_affine(p + ".shortcut.1", ss, hs);
+          const std::vector<float>& w3 = P(p + ".conv3.weight");
+          const std::vector<float>& wsc = P(p + ".shortcut.0.weight");
+          const int K = rb.planes + rb.in_planes, N = rb.out_planes;
+          std::vector<float> wf((size_t)N * K), bf(N);
+          for (int n = 0; n < N; ++n) {
+            for (int k = 0; k < rb.planes; ++k) wf[(size_t)n * K + k] = (float)(w3[(size_t)n * rb.planes + k] * s3[n]);
+            for (int k = 0; k < rb.in_planes; ++k)
+              wf[(size_t)n * K + rb.planes + k] = (float)(wsc[(size_t)n * rb.in_planes + k] * ss[n]);
+            bf[n] = (float)h3[n] + (float)hs[n];
+          }
+          rb.c3sc = pack_conv(wf, N, K, 1, bf.data(), "");
+        }
       }
     // seg_1 over TSTP stats; reference flatten index s*C*F4 + c*F4 + f, ours f*2C + s*C + c
     const int C4 = rblocks.back().out_planes, F4 = feat_dim / 8;
@@ -657,6 +678,31 @@ struct Model::Impl {
     run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant, s); });
   }
 
+  // bottleneck conv3 + projection shortcut as one GEMM (RBlock::c3sc, ConvGemmArgs::sc2d): A segment 0
+  // = y2 [M][planes] (row m), segment 1 = the block input x [B][Fi][Ti][Ci] at the shortcut's
+  // strided position of output row m
+  void gemm_c3sc(const char* tag, const RBlock& rb, const float* y2, const float* x, int Ci, float* out, int B,
+                 int Fi, int Ti, int Fo, int To, hipStream_t s) {
+    const ConvW& cw = rb.c3sc;
+    ConvGemmArgs g{};
+    g.a[0] = y2;
+    g.a[1] = g.a[2] = x;
+    g.lda[0] = rb.planes;
+    g.lda[1] = g.lda[2] = Ci;
+    g.cseg[0] = 0;
+    g.cseg[1] = rb.planes;
+    g.cseg[2] = g.cseg[3] = cw.cin;
+    const int M = B * Fo * To;
+    fill(g, cw, M, M, 1, 0, out, cw.N, kActRelu, nullptr, true);
+    g.sc2d = 1;
+    g.Fi = Fi;
+    g.Ti = Ti;
+    g.Fo = Fo;
+    g.To = To;
+    g.stride = rb.stride;
+    run(tag, 2.0 * M * cw.N * cw.K, s, [&] { launch_conv_gemm_x3(g, cw.whi, cw.wlo, x3_variant, s); });
+  }
+
   void forward_resnet(const float* feats, int B, int T, float* embed, float* ws, hipStream_t s) {
     const int bc = resnet_chunk(B, T);
     size_t off[6];
@@ -691,7 +737,10 @@ struct Model::Impl {
         ++ib;
         const int Fo = (Fi - 1) / rb.stride + 1, To = (Ti - 1) / rb.stride + 1;
         const float* res = x;
-        if (rb.has_sc) {
+        const bool tail = bottleneck && rb.stride == 1 && res_tail && rb.w3acc && img_ok(rb.c2, rb.planes);
+        // conv3 + shortcut in one GEMM on the non-tail path (sc_fuse): no SC round trip through HBM
+        const bool fuse_sc = bottleneck && rb.has_sc && !tail && sc_fuse && rb.c3sc.w && x3_variant == 7;
+        if (rb.has_sc && !fuse_sc) {
           gemm2d("shortcut", rb.sc, x, Ci, SC, rb.out_planes, nb, Fi, Ti, 1, rb.stride, 0, kActNone, nullptr, 0, s);
           res = SC;
         }
@@ -699,7 +748,7 @@ struct Model::Impl {
           if (!y1_ready) gemm1x1(kC1[li], rb.c1, x, Y1, nb * Fi * Ti, kActRelu, nullptr, s);
           const float* y1 = y1_ready ? y1_next : Y1;
           y1_ready = false;
-          if (rb.stride == 1 && res_tail && rb.w3acc && img_ok(rb.c2, rb.planes)) {
+          if (tail) {
             // conv2 + conv3 + residual in one launch, y2 in registers (bottleneck_tail); with
             // res_tail 1 also the next block's conv1 on this block's output (into the buffer
             // the tail does not read)
@@ -730,7 +779,10 @@ struct Model::Impl {
               gemm2d(kK3[li], rb.c2, Y1, rb.planes, Y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0,
                      s);
             }
-            gemm1x1(kC3[li], rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
+            if (fuse_sc)
+              gemm_c3sc(kC3[li], rb, Y2, x, Ci, o, nb, Fi, Ti, Fo, To, s);
+            else
+              gemm1x1(kC3[li], rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
           }
         } else {
           if (rb.stride == 1 && img_ok(rb.c1, rb.planes)) {
