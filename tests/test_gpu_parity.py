@@ -137,6 +137,26 @@ def test_resnet_fused_conv3_shortcut(arch, B, T, res_tail):
     assert float((fused - split).abs().max()) <= 1e-5 * max(1.0, float(split.abs().max()))
 
 
+@pytest.mark.parametrize("arch,B,T", [("ResNet50", 2, 131), ("ResNet293", 2, 64)])
+def test_resnet_stage_transition_conv1_in_tail(arch, B, T):
+    """A stage's first conv1 (4C -> 2C, C = 32 / 64) computed inside the previous stage's last
+    fused tail (tail2_kernel R1 = 2, option c1_stage_fuse): against the oracle, and against the
+    separate 1x1 GEMM (c1_stage_fuse 0) within the MFMA-shape summation-order difference."""
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    m = HipSpeakerModel(arch, feat_dim=80, embed_dim=256)
+    sd = synth_state_dict(31, m.state_dict_layout(), residual_tame=True)
+    m.load_state_dict(sd)
+    m.to(DEV)
+    x = torch.from_numpy(synth_feats(95, B, T, 80)).to(DEV)
+    _, fused = m(x)
+    m.set_option("c1_stage_fuse", 0)
+    _, split = m(x)
+    with torch.no_grad():
+        _, ref = models_ref.forward(arch, x.cpu(), {k: torch.from_numpy(v) for k, v in sd.items()})
+    _assert_emb(fused.cpu().numpy(), ref.numpy())
+    assert float((fused - split).abs().max()) <= 1e-5 * max(1.0, float(split.abs().max()))
+
+
 @pytest.mark.parametrize("feat_dim", [136, 72])
 def test_resnet_split_k_head_partial_slice(feat_dim):
     """The TSTP head's split-K linear (ops.hip small_linear_splitk_kernel, K >= 4096): feat_dim 136

@@ -49,6 +49,9 @@ struct BottleneckTailArgs {
   const void* w1n = nullptr;
   const float* b1n = nullptr;
   float* y1n = nullptr;
+  // the next conv1's output channels: C, or 2C at a stage transition (the next stage's first
+  // block: 4C -> 2C, y1n [B][F][T][2C]; 32 / 64 planes); 0 = C
+  int c1n = 0;
 };
 bool bottleneck_tail_supported(int C);
 void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s);

@@ -531,19 +531,21 @@ constexpr int tail2_lds() {
   return Img<C, FB, 32>::LDS > need ? Img<C, FB, 32>::LDS : need;
 }
 
-template <int C, int P1, int RD3, int RD1, int FB = tail2_fb<C>(), int MINB = 2>
+// R1: the next conv1's output channels in units of C (2 at a stage transition: wave g computes
+// conv1 output tiles g and g + GW)
+template <int C, int P1, int RD3, int RD1, int FB = tail2_fb<C>(), int MINB = 2, int R1 = 1>
 __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailArgs p) {
   constexpr int TB = 32;
   using G = Img<C, FB, TB, 1, 4>;  // patch image staged by the 4 waves
   constexpr int PT = G::PT, CT = G::CT, KS = G::KS;
   // runs; runs per wave (a pair, or the block's one run); column groups per wave's runs
   constexpr int NR = FB, RW = NR >= 2 ? 2 : 1, GW = 4 * RW / NR;
-  constexpr int C4 = 4 * C, NT3 = C4 / 32, KS3 = C / 16, NT1 = C / 32;
+  constexpr int C4 = 4 * C, NT3 = C4 / 32, KS3 = C / 16, NT1 = R1 * C / 32, C1N = R1 * C;
   constexpr int NCHK = NT3 / GW, KB = 2 * GW;    // chunks of GW tiles; conv1 k-steps per chunk
   constexpr int Y2B = NR * KS3 * 2048;           // y2 fragments of every run
   constexpr int CBR = GW * 64, CBP = NR * 32 * CBR;  // chunk buffer: NR x 32 rows x GW x 32 bf16 per plane
   constexpr int CBLO = CBP + 64;                 // lo plane 64 B off: paired hi / lo stores, distinct banks
-  static_assert(G::NT == 256 && CT == GW && NT1 == GW && KS % P1 == 0 && P1 % 2 == 0, "tail2: wave layout");
+  static_assert(G::NT == 256 && CT == GW && NT1 == R1 * GW && KS % P1 == 0 && P1 % 2 == 0, "tail2: wave layout");
   static_assert(KS3 % RD3 == 0 && RD1 >= 1 && RD1 + 1 <= KB, "tail2: ring depths");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* xhi = smem;
@@ -673,14 +675,14 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
     bh = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3, c < NCHK ? o : kOOB, 0, 0));
     bl = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3, c < NCHK ? o + NT3 * 1024 : kOOB, 0, 0));
   };
-  auto w1load = [&](int ks, bf16x8& bh, bf16x8& bl) {
-    const int o = ((ks * 2 * NT1 + g) * 64 + lane) * 16;
+  auto w1load = [&](int ks, int j, bf16x8& bh, bf16x8& bl) {  // conv1 output tile g + GW j
+    const int o = ((ks * 2 * NT1 + g + GW * j) * 64 + lane) * 16;
     bh = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1, o, 0, 0));
     bl = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1, o + NT1 * 1024, 0, 0));
   };
   // W3 / W1 rings (slot j = k-step j mod RD3 / RD1); chunk 0's first RD3 W3 k-steps go out
   // before the y2 conversion
-  bf16x8 ch_[RD3], cl_[RD3], uh_[RD1], ul_[RD1];
+  bf16x8 ch_[RD3], cl_[RD3], uh_[RD1][R1], ul_[RD1][R1];
 #pragma unroll
   for (int j = 0; j < RD3; ++j) w3load(0, j, ch_[j], cl_[j]);
 
@@ -748,15 +750,19 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
     }
   };
 
-  f32x16 acc1[RW], a3[RW];
+  f32x16 acc1[R1][RW], a3[RW];
 #pragma unroll
-  for (int i = 0; i < RW; ++i)
+  for (int j = 0; j < R1; ++j)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc1[i][r] = 0.f;
+    for (int i = 0; i < RW; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc1[j][i][r] = 0.f;
 #pragma unroll 1
   for (int c = 0; c < NCHK; ++c) {
 #pragma unroll
-    for (int j = 0; j < RD1; ++j) w1load(KB * c + j, uh_[j], ul_[j]);  // land during the chunk's conv3
+    for (int j = 0; j < RD1; ++j)  // land during the chunk's conv3
+#pragma unroll
+      for (int u = 0; u < R1; ++u) w1load(KB * c + j, u, uh_[j][u], ul_[j][u]);
     // conv3, column tile GW c + g, the wave's two runs
 #pragma unroll
     for (int i = 0; i < RW; ++i)
@@ -816,26 +822,32 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
     for (int kk = 0; kk < KB; ++kk) {
       if (kk + 1 < KB) read_cb(kk + 1, ah[(kk + 1) & 1], al[(kk + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      mma2(acc1, ah[kk & 1], al[kk & 1], uh_[kk % RD1], ul_[kk % RD1]);
-      if (kk + RD1 < KB) w1load(KB * c + kk + RD1, uh_[kk % RD1], ul_[kk % RD1]);
+#pragma unroll
+      for (int u = 0; u < R1; ++u) mma2(acc1[u], ah[kk & 1], al[kk & 1], uh_[kk % RD1][u], ul_[kk % RD1][u]);
+#pragma unroll
+      for (int u = 0; u < R1; ++u)
+        if (kk + RD1 < KB) w1load(KB * c + kk + RD1, u, uh_[kk % RD1][u], ul_[kk % RD1][u]);
       if (kk + RD1 + 1 == KB) rload(c + 1, c + 1 < NCHK);  // right behind the chunk's last W1 fetch
       __builtin_amdgcn_sched_barrier(0);
     }
     WSP_TAIL_STAMP(4 + c);
   }
-  // y1' = relu(acc1 + b1') -> y1n [B][F][T][C], output tile g
+  // y1' = relu(acc1 + b1') -> y1n [B][F][T][C1N], output tiles g + GW j
   {
-    const __amdgpu_buffer_rsrc_t ry = make_rsrc(p.y1n + (size_t)b * plane * C);
-    const int col = g * 32 + r32;
-    const float bv = p.b1n[col];
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc(p.y1n + (size_t)b * plane * C1N);
 #pragma unroll
-    for (int i = 0; i < RW; ++i) {
-      const int lim = rlim(i, true);
+    for (int u = 0; u < R1; ++u) {
+      const int col = (g + GW * u) * 32 + r32;
+      const float bv = p.b1n[col];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float y = fmaxf(acc1[i][r] + bv, 0.f);
-        const unsigned o = (((unsigned)(fw + i) * p.T + tw + tro(r)) * C + col) * 4;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ry, tro(r) < lim ? (int)o : kOOB, 0, 0);
+      for (int i = 0; i < RW; ++i) {
+        const int lim = rlim(i, true);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float y = fmaxf(acc1[u][i][r] + bv, 0.f);
+          const unsigned o = (((unsigned)(fw + i) * p.T + tw + tro(r)) * C1N + col) * 4;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ry, tro(r) < lim ? (int)o : kOOB, 0, 0);
+        }
       }
     }
   }
@@ -885,10 +897,11 @@ void launch_tail_k(const BottleneckTailArgs& p, hipStream_t s) {
   hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB, NC, P1, PM>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
 }
 
-template <int C, int P1, int RD3, int RD1, int FB = tail2_fb<C>(), int MINB = 2>
+template <int C, int P1, int RD3, int RD1, int FB = tail2_fb<C>(), int MINB = 2, int R1 = 1>
 void launch_tail2(const BottleneckTailArgs& p, hipStream_t s) {
   const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + 31) / 32);
-  hipLaunchKernelGGL((tail2_kernel<C, P1, RD3, RD1, FB, MINB>), dim3(nblk), dim3(256), (tail2_lds<C, FB>()), s, p);
+  hipLaunchKernelGGL((tail2_kernel<C, P1, RD3, RD1, FB, MINB, R1>), dim3(nblk), dim3(256), (tail2_lds<C, FB>()), s,
+                     p);
 }
 }  // namespace
 
@@ -903,12 +916,19 @@ void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s) {
   WSP_CHECK((long long)p.F * p.T * 4 * C * 4 < (long long)kOOB, "bottleneck_tail: utterance exceeds 2 GiB");
   WSP_CHECK(!p.w1n || (p.b1n && p.y1n && p.y1n != p.out && p.y1n != p.y1 && p.y1n != p.res),
             "bottleneck_tail: next conv1 needs bias and a separate output");
+  WSP_CHECK(p.c1n == 0 || p.c1n == C || (p.c1n == 2 * C && p.w1n && C <= 64),
+            "bottleneck_tail: the next conv1 is C -> C, or C -> 2C with 32 / 64 planes");
   if (p.w1n) {  // with the next block's conv1: every wave on two position runs (tail2_kernel)
     // <C, W2 ring depth, W3 ring, W1 ring>; 128 planes with an 8-deep W2 ring: 0.323 -> 0.314 ms
     // per launch (tools/tail_check, B = 64, interleaved rounds); deeper W2 / W1 rings for 32 / 64
     // planes measured within 0.5 %
-    if (C == 32)
+    const bool wide = p.c1n == 2 * C;  // stage transition: the next conv1 is 4C -> 2C
+    if (C == 32 && wide)
+      launch_tail2<32, 2, 2, 1, tail2_fb<32>(), 2, 2>(p, s);
+    else if (C == 32)
       launch_tail2<32, 2, 2, 1>(p, s);  // 8 x 32 positions, 4 waves, 64 KB: 2 blocks / CU
+    else if (C == 64 && wide)
+      launch_tail2<64, 4, 4, 2, tail2_fb<64>(), 2, 2>(p, s);
     else if (C == 64)
       launch_tail2<64, 4, 4, 2>(p, s);  // 4 x 32 positions, 64 KB
     else

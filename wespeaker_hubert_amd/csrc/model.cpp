@@ -240,6 +240,9 @@ void Model::set_option(const std::string& key, int value) {
   } else if (key == "res_prefetch") {
     WSP_CHECK(value == 0 || value == 1, "res_prefetch must be 0 or 1");
     impl->res_prefetch = value;
+  } else if (key == "c1_stage_fuse") {
+    WSP_CHECK(value == 0 || value == 1, "c1_stage_fuse must be 0 or 1");
+    impl->c1_stage_fuse = value;
   } else if (key == "sc_fuse") {
     WSP_CHECK(value == 0 || value == 1, "sc_fuse must be 0 or 1");
     impl->sc_fuse = value;
@@ -302,6 +305,7 @@ int Model::get_option(const std::string& key) const {
   if (key == "res_prefetch") return m.res_prefetch;
   if (key == "res_tail") return m.res_tail;
   if (key == "sc_fuse") return m.sc_fuse;
+  if (key == "c1_stage_fuse") return m.c1_stage_fuse;
   if (key == "astp_fused") return m.astp_fused_on;
   if (key == "attn_pipe") return m.attn_pipe;
   if (key == "pos_conv") return m.pos_conv;

@@ -157,6 +157,7 @@ struct Model::Impl {
   // per wave), 2 = the tail alone, 0 = off
   int res_tail = 1;
   int sc_fuse = 1;  // bottleneck conv3 + projection shortcut as one GEMM (RBlock::c3sc)
+  int c1_stage_fuse = 1;  // a stage's first conv1 (4C -> 2C) inside the previous stage's last tail
   bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
   int res2_variant = 4;  // res2_chain.hip kernel variant (option "res2_variant"; 4 = halo-free strips, C2 1.48 -> 1.24 ms/step; c512 widths run 3)
   ConvW conv, pool1, pool2;
@@ -535,8 +536,12 @@ struct Model::Impl {
         if (bottleneck) {
           // a stride-1 block whose input has 4 x its planes (every block after the first of a
           // stage) runs its conv1 inside the previous block's bottleneck_tail
-          const bool c1_in_tail = rb.stride == 1 && rb.in_planes == 4 * rb.planes && bi > 0 &&
-                                  bottleneck_tail_supported(rb.planes);
+          // ... and a stage's first block whose conv1 is 2C <- 4C of the previous stage's C = 32 / 64
+          // planes runs it inside the previous stage's last tail (c1_stage_fuse)
+          const bool c1_in_tail = (rb.stride == 1 && rb.in_planes == 4 * rb.planes && bi > 0 &&
+                                   bottleneck_tail_supported(rb.planes)) ||
+                                  (bi == 0 && li > 0 && rb.in_planes == 2 * rb.planes && rb.planes <= 128 &&
+                                   bottleneck_tail_supported(rb.planes / 2));
           rb.c1 = pack_conv_bn(p + ".conv1.weight", p + ".bn1", rb.planes, rb.in_planes, 1, nullptr,
                                c1_in_tail ? &rb.w1frag : nullptr);
           rb.c2 = pack_conv_bn(p + ".conv2.weight", p + ".bn2", rb.planes, rb.planes, 9);
@@ -610,6 +615,9 @@ struct Model::Impl {
       r.big = std::max(r.big, (size_t)Fo * To * rb.out_planes);
       r.y1 = std::max(r.y1, (size_t)(bottleneck ? Fi * Ti : Fo * To) * rb.planes);
       r.y2 = std::max(r.y2, (size_t)Fo * To * rb.planes);
+      // the buffers Y1 / Y2 alternate as a fused tail's input and its next-conv1 output, which at a
+      // stage transition is the next stage's conv1 at this resolution
+      if (bottleneck) r.y2 = std::max(r.y2, (size_t)Fi * Ti * rb.planes);
       if (rb.has_sc) r.sc = std::max(r.sc, (size_t)Fo * To * rb.out_planes);
       Fi = Fo;
       Ti = To;
@@ -753,15 +761,19 @@ struct Model::Impl {
             // res_tail 1 also the next block's conv1 on this block's output (into the buffer
             // the tail does not read)
             const RBlock* nx = (size_t)ib < rblocks.size() ? &rblocks[ib] : nullptr;
-            // (the next block must run the tail too: its conv2 then reads y1 from either buffer)
-            const bool fuse1 = res_tail == 1 && nx && nx->w1frag && nx->planes == rb.planes && nx->w3acc &&
-                               nx->stride == 1 && img_ok(nx->c2, nx->planes);
+            // (the next block's conv2 reads y1 from either buffer); at a stage transition the next
+            // (first) block's conv1 is 4C -> 2C at this stage's resolution (option c1_stage_fuse)
+            const bool fuse1 =
+                res_tail == 1 && nx && nx->w1frag &&
+                ((nx->planes == rb.planes && nx->w3acc && nx->stride == 1 && img_ok(nx->c2, nx->planes)) ||
+                 (c1_stage_fuse && nx->planes == 2 * rb.planes && nx->in_planes == rb.out_planes && rb.planes <= 64));
             BottleneckTailArgs a{y1, res, o, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.w3acc, rb.c3.bias};
             float* y1n = y1 == Y1 ? Y2 : Y1;
             if (fuse1) {
               a.w1n = nx->w1frag;
               a.b1n = nx->c1.bias;
               a.y1n = y1n;
+              a.c1n = nx->planes;
             }
             const double pos = (double)nb * Fi * Ti;
             run(kTl[li], 2.0 * pos * (rb.c2.N * rb.c2.K + rb.c3.N * rb.c3.K + (fuse1 ? nx->c1.N * nx->c1.K : 0)), s,
@@ -771,18 +783,20 @@ struct Model::Impl {
               y1_next = y1n;
             }
           } else {
+            // y1 is in Y1, or in Y2 when the previous block's tail computed this conv1
+            float* y2 = y1 == Y2 ? Y1 : Y2;
             if (rb.stride == 1 && img_ok(rb.c2, rb.planes)) {
-              const Conv3x3Args a{Y1, Y2, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, nullptr, 1,
+              const Conv3x3Args a{y1, y2, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.c2.scale, rb.c2.shift, nullptr, 1,
                                   conv3x3_img_on};
               run(kK3[li], 2.0 * nb * Fi * Ti * rb.c2.N * rb.c2.K, s, [&] { launch_conv3x3_img(a, rb.planes, s); });
             } else {
-              gemm2d(kK3[li], rb.c2, Y1, rb.planes, Y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0,
+              gemm2d(kK3[li], rb.c2, y1, rb.planes, y2, rb.planes, nb, Fi, Ti, 3, rb.stride, 1, kActRelu, nullptr, 0,
                      s);
             }
             if (fuse_sc)
-              gemm_c3sc(kC3[li], rb, Y2, x, Ci, o, nb, Fi, Ti, Fo, To, s);
+              gemm_c3sc(kC3[li], rb, y2, x, Ci, o, nb, Fi, Ti, Fo, To, s);
             else
-              gemm1x1(kC3[li], rb.c3, Y2, o, nb * Fo * To, kActRelu, res, s);
+              gemm1x1(kC3[li], rb.c3, y2, o, nb * Fo * To, kActRelu, res, s);
           }
         } else {
           if (rb.stride == 1 && img_ok(rb.c1, rb.planes)) {
