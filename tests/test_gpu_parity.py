@@ -137,6 +137,28 @@ def test_resnet_fused_conv3_shortcut(arch, B, T, res_tail):
     assert float((fused - split).abs().max()) <= 1e-5 * max(1.0, float(split.abs().max()))
 
 
+@pytest.mark.parametrize("B,T", [(3, 45), (1, 200)])
+def test_resnet_shortcut_in_tail(B, T):
+    """layer1.0's projection shortcut (32 -> 128, stride 1) as extra conv3 k-steps inside the
+    fused tail, x's fragments in registers (tail2_kernel SCX, BottleneckTailArgs::xsc): against
+    the oracle, and against the shortcut GEMM + residual read (sc_fuse 0); ragged T (45: a
+    partial 32-position tile)."""
+    from wespeaker_hubert_amd.speaker_model import HipSpeakerModel
+    m = HipSpeakerModel("ResNet50", feat_dim=80, embed_dim=256)
+    sd = synth_state_dict(37, m.state_dict_layout(), residual_tame=True)
+    m.load_state_dict(sd)
+    m.to(DEV)
+    m.set_option("res_tail", 1)
+    x = torch.from_numpy(synth_feats(93, B, T, 80)).to(DEV)
+    _, fused = m(x)
+    m.set_option("sc_fuse", 0)
+    _, split = m(x)
+    with torch.no_grad():
+        _, ref = models_ref.forward("ResNet50", x.cpu(), {k: torch.from_numpy(v) for k, v in sd.items()})
+    _assert_emb(fused.cpu().numpy(), ref.numpy())
+    assert float((fused - split).abs().max()) <= 1e-5 * max(1.0, float(split.abs().max()))
+
+
 @pytest.mark.parametrize("arch,B,T", [("ResNet50", 2, 131), ("ResNet293", 2, 64)])
 def test_resnet_stage_transition_conv1_in_tail(arch, B, T):
     """A stage's first conv1 (4C -> 2C, C = 32 / 64) computed inside the previous stage's last

@@ -52,6 +52,10 @@ struct BottleneckTailArgs {
   // the next conv1's output channels: C, or 2C at a stage transition (the next stage's first
   // block: 4C -> 2C, y1n [B][F][T][2C]; 32 / 64 planes); 0 = C
   int c1n = 0;
+  // optional (32 planes, with w1n): the block's projection shortcut computed inside conv3 from its
+  // input x [B][F][T][C] (C -> 4C; w3 then holds KS3 more k-steps, natural k order, and b3 = b3 +
+  // b_sc); res must be null
+  const float* xsc = nullptr;
 };
 bool bottleneck_tail_supported(int C);
 void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s);

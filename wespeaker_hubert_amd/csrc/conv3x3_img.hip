@@ -532,8 +532,10 @@ constexpr int tail2_lds() {
 }
 
 // R1: the next conv1's output channels in units of C (2 at a stage transition: wave g computes
-// conv1 output tiles g and g + GW)
-template <int C, int P1, int RD3, int RD1, int FB = tail2_fb<C>(), int MINB = 2, int R1 = 1>
+// conv1 output tiles g and g + GW).  SCX: the block's projection shortcut (C -> 4C, its input x
+// of C channels at the output positions: a stage's stride-1 first block) as KS3 more conv3
+// k-steps with x's fragments in registers, instead of a residual read (BottleneckTailArgs::xsc)
+template <int C, int P1, int RD3, int RD1, int FB = tail2_fb<C>(), int MINB = 2, int R1 = 1, bool SCX = false>
 __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailArgs p) {
   constexpr int TB = 32;
   using G = Img<C, FB, TB, 1, 4>;  // patch image staged by the 4 waves
@@ -541,12 +543,13 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
   // runs; runs per wave (a pair, or the block's one run); column groups per wave's runs
   constexpr int NR = FB, RW = NR >= 2 ? 2 : 1, GW = 4 * RW / NR;
   constexpr int C4 = 4 * C, NT3 = C4 / 32, KS3 = C / 16, NT1 = R1 * C / 32, C1N = R1 * C;
+  constexpr int KT3 = SCX ? 2 * KS3 : KS3;  // conv3 k-steps: y2, then (SCX) the shortcut's x
   constexpr int NCHK = NT3 / GW, KB = 2 * GW;    // chunks of GW tiles; conv1 k-steps per chunk
   constexpr int Y2B = NR * KS3 * 2048;           // y2 fragments of every run
   constexpr int CBR = GW * 64, CBP = NR * 32 * CBR;  // chunk buffer: NR x 32 rows x GW x 32 bf16 per plane
   constexpr int CBLO = CBP + 64;                 // lo plane 64 B off: paired hi / lo stores, distinct banks
   static_assert(G::NT == 256 && CT == GW && NT1 == R1 * GW && KS % P1 == 0 && P1 % 2 == 0, "tail2: wave layout");
-  static_assert(KS3 % RD3 == 0 && RD1 >= 1 && RD1 + 1 <= KB, "tail2: ring depths");
+  static_assert(KS3 % RD3 == 0 && KT3 % RD3 == 0 && RD1 >= 1 && RD1 + 1 <= KB, "tail2: ring depths");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* xhi = smem;
   unsigned char* xlo = smem + G::PLANE;
@@ -596,12 +599,14 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
   auto rload = [&](int c, bool live) {  // !live: the same loads, out of range (branch-free count)
     const int col = (GW * c + g) * 32 + r32;
     b3v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb3, live ? col * 4 : kOOB, 0, 0));
+    if constexpr (!SCX) {
 #pragma unroll
-    for (int i = 0; i < RW; ++i) {
-      const int lim = rlim(i, live);
+      for (int i = 0; i < RW; ++i) {
+        const int lim = rlim(i, live);
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        rv[i][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, roff(i, col, r, lim), 0, 0));
+        for (int r = 0; r < 16; ++r)
+          rv[i][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, roff(i, col, r, lim), 0, 0));
+      }
     }
   };
 
@@ -685,6 +690,28 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
   bf16x8 ch_[RD3], cl_[RD3], uh_[RD1][R1], ul_[RD1][R1];
 #pragma unroll
   for (int j = 0; j < RD3; ++j) w3load(0, j, ch_[j], cl_[j]);
+  // SCX: the shortcut input's A fragments, natural k order (lane: position t0 + r32 of run i,
+  // channels 16 ks + 8 h .. + 7), split into bf16 hi / lo once for every chunk
+  bf16x8 xsh[SCX ? KS3 : 1][RW], xsl[SCX ? KS3 : 1][RW];
+  if constexpr (SCX) {
+    const __amdgpu_buffer_rsrc_t rxs = make_rsrc(p.xsc + (size_t)b * plane * C);
+#pragma unroll
+    for (int ks = 0; ks < KS3; ++ks)
+#pragma unroll
+      for (int i = 0; i < RW; ++i) {
+        const bool ok = fw + i < p.F && t0 + r32 < p.T;
+        const unsigned o = (((unsigned)(fw + i) * p.T + t0 + r32) * C + 16 * ks + 8 * h) * 4;
+        const f32x4 v0 = bload4(rxs, ok ? (int)o : kOOB), v1 = bload4(rxs, ok ? (int)(o + 16) : kOOB);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const __bf16 h0 = (__bf16)v0[e], h1 = (__bf16)v1[e];
+          xsh[ks][i][e] = h0;
+          xsh[ks][i][4 + e] = h1;
+          xsl[ks][i][e] = (__bf16)(v0[e] - (float)h0);
+          xsl[ks][i][4 + e] = (__bf16)(v1[e] - (float)h1);
+        }
+      }
+  }
 
   // ---- y2 = relu(acc + b2) -> LDS fragments [run][k-step][hi, lo][lane] (k-step 2 g + s2 =
   // registers 8 s2 .. 8 s2 + 7 of channel tile g)
@@ -771,12 +798,15 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
     bf16x8 ah[2][RW], al[2][RW];
     read_y2(0, ah[0], al[0]);
 #pragma unroll
-    for (int q = 0; q < KS3; ++q) {
+    for (int q = 0; q < KT3; ++q) {
       if (q + 1 < KS3) read_y2(q + 1, ah[(q + 1) & 1], al[(q + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      mma2(a3, ah[q & 1], al[q & 1], ch_[q % RD3], cl_[q % RD3]);
-      if (q + RD3 < KS3) w3load(c, q + RD3, ch_[q % RD3], cl_[q % RD3]);
-      else w3load(c + 1, q + RD3 - KS3, ch_[q % RD3], cl_[q % RD3]);
+      if (q < KS3)
+        mma2(a3, ah[q & 1], al[q & 1], ch_[q % RD3], cl_[q % RD3]);
+      else
+        mma2(a3, xsh[q < KS3 ? 0 : q - KS3], xsl[q < KS3 ? 0 : q - KS3], ch_[q % RD3], cl_[q % RD3]);
+      if (q + RD3 < KT3) w3load(c, q + RD3, ch_[q % RD3], cl_[q % RD3]);
+      else w3load(c + 1, q + RD3 - KT3, ch_[q % RD3], cl_[q % RD3]);
       __builtin_amdgcn_sched_barrier(0);
     }
     if (c == 1) WSP_TAIL_STAMP(8);
@@ -795,7 +825,7 @@ __global__ __launch_bounds__(256, MINB) void tail2_kernel(const BottleneckTailAr
         const int lim = rlim(i, true);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float y = fmaxf(a3[i][r] + b3v + rv[i][r], 0.f);
+          const float y = SCX ? fmaxf(a3[i][r] + b3v, 0.f) : fmaxf(a3[i][r] + b3v + rv[i][r], 0.f);
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ro, roff(i, col, r, lim), 0, 0);
           // lanes l, l ^ 1 hold columns c, c ^ 1: the even lane stores both hi halves, the odd
           // lane both lo halves — one 4-B store per lane at a lane-parity plane offset, the word
@@ -897,11 +927,11 @@ void launch_tail_k(const BottleneckTailArgs& p, hipStream_t s) {
   hipLaunchKernelGGL((bottleneck_tail_kernel<C, FB, TB, WN, MINB, NC, P1, PM>), dim3(nblk), dim3(G::NT), G::LDS, s, p);
 }
 
-template <int C, int P1, int RD3, int RD1, int FB = tail2_fb<C>(), int MINB = 2, int R1 = 1>
+template <int C, int P1, int RD3, int RD1, int FB = tail2_fb<C>(), int MINB = 2, int R1 = 1, bool SCX = false>
 void launch_tail2(const BottleneckTailArgs& p, hipStream_t s) {
   const int nblk = p.B * ((p.F + FB - 1) / FB) * ((p.T + 31) / 32);
-  hipLaunchKernelGGL((tail2_kernel<C, P1, RD3, RD1, FB, MINB, R1>), dim3(nblk), dim3(256), (tail2_lds<C, FB>()), s,
-                     p);
+  hipLaunchKernelGGL((tail2_kernel<C, P1, RD3, RD1, FB, MINB, R1, SCX>), dim3(nblk), dim3(256), (tail2_lds<C, FB>()),
+                     s, p);
 }
 }  // namespace
 
@@ -909,7 +939,7 @@ bool bottleneck_tail_supported(int C) { return C == 32 || C == 64 || C == 128; }
 
 void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s) {
   WSP_CHECK(bottleneck_tail_supported(C), "bottleneck_tail: planes must be 32, 64 or 128");
-  WSP_CHECK(p.B > 0 && p.F > 0 && p.T > 0 && p.y1 && p.res && p.out && p.w2 && p.w3 && p.b2 && p.b3,
+  WSP_CHECK(p.B > 0 && p.F > 0 && p.T > 0 && p.y1 && (p.res || p.xsc) && p.out && p.w2 && p.w3 && p.b2 && p.b3,
             "bottleneck_tail: bad arguments");
   WSP_CHECK(p.out != p.res && p.out != p.y1, "bottleneck_tail: out must not alias its inputs");
   // buffer offsets are per utterance (descriptors based at its first element)
@@ -918,12 +948,16 @@ void launch_bottleneck_tail(const BottleneckTailArgs& p, int C, hipStream_t s) {
             "bottleneck_tail: next conv1 needs bias and a separate output");
   WSP_CHECK(p.c1n == 0 || p.c1n == C || (p.c1n == 2 * C && p.w1n && C <= 64),
             "bottleneck_tail: the next conv1 is C -> C, or C -> 2C with 32 / 64 planes");
+  WSP_CHECK(!p.xsc || (C == 32 && p.w1n && !p.res && (p.c1n == 0 || p.c1n == C) && p.xsc != p.out),
+            "bottleneck_tail: the in-tail shortcut needs 32 planes, the fused next conv1 and no residual");
   if (p.w1n) {  // with the next block's conv1: every wave on two position runs (tail2_kernel)
     // <C, W2 ring depth, W3 ring, W1 ring>; 128 planes with an 8-deep W2 ring: 0.323 -> 0.314 ms
     // per launch (tools/tail_check, B = 64, interleaved rounds); deeper W2 / W1 rings for 32 / 64
     // planes measured within 0.5 %
     const bool wide = p.c1n == 2 * C;  // stage transition: the next conv1 is 4C -> 2C
-    if (C == 32 && wide)
+    if (p.xsc)  // the stage's stride-1 first block with its shortcut inside conv3 (32 planes)
+      launch_tail2<32, 2, 2, 1, tail2_fb<32>(), 2, 1, true>(p, s);
+    else if (C == 32 && wide)
       launch_tail2<32, 2, 2, 1, tail2_fb<32>(), 2, 2>(p, s);
     else if (C == 32)
       launch_tail2<32, 2, 2, 1>(p, s);  // 8 x 32 positions, 4 waves, 64 KB: 2 blocks / CU

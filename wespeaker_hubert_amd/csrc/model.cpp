@@ -244,7 +244,7 @@ void Model::set_option(const std::string& key, int value) {
     WSP_CHECK(value == 0 || value == 1, "c1_stage_fuse must be 0 or 1");
     impl->c1_stage_fuse = value;
   } else if (key == "sc_fuse") {
-    WSP_CHECK(value == 0 || value == 1, "sc_fuse must be 0 or 1");
+    WSP_CHECK(value >= 0 && value <= 3, "sc_fuse must be 0 .. 3 (bit 0: one GEMM, bit 1: in the tail)");
     impl->sc_fuse = value;
   } else if (key == "res_tail") {
     WSP_CHECK(value >= 0 && value <= 2, "res_tail must be 0 (off), 1 (tail + next conv1) or 2 (tail alone)");

@@ -156,7 +156,9 @@ struct Model::Impl {
   // next block's conv1 on the tail's output while it is on chip (tail2_kernel: two position runs
   // per wave), 2 = the tail alone, 0 = off
   int res_tail = 1;
-  int sc_fuse = 1;  // bottleneck conv3 + projection shortcut as one GEMM (RBlock::c3sc)
+  // bottleneck conv3 + projection shortcut fused: bit 0 as one GEMM (RBlock::c3sc), bit 1 inside
+  // the fused tail (RBlock::w3scx)
+  int sc_fuse = 3;
   int c1_stage_fuse = 1;  // a stage's first conv1 (4C -> 2C) inside the previous stage's last tail
   bool img_ok(const ConvW& cw, int C) const { return cw.frag && conv3x3_img_on && (C <= 64 || conv3x3_img_on >= 2); }
   int res2_variant = 4;  // res2_chain.hip kernel variant (option "res2_variant"; 4 = halo-free strips, C2 1.48 -> 1.24 ms/step; c512 widths run 3)
@@ -186,6 +188,10 @@ struct Model::Impl {
     // through HBM (option "sc_fuse"; bottleneck blocks off the fused-tail path, N % 256 == 0)
     ConvW c3sc;
     void* w3acc = nullptr;  // conv3 (bn3 folded) as pack_frag_acc B fragments for bottleneck_tail
+    // [conv3 | shortcut] (both BN-folded) for the in-tail shortcut (BottleneckTailArgs::xsc) and its
+    // summed bias: a stride-1 first block with in_planes == planes == 32
+    void* w3scx = nullptr;
+    float* b3scx = nullptr;
     void* w1frag = nullptr;  // conv1 (bn1 folded) as pack_frag B fragments: run inside the previous block's tail
     bool has_sc = false;
     int stride = 1, in_planes = 0, planes = 0, out_planes = 0;
@@ -377,14 +383,17 @@ struct Model::Impl {
   // + 4 (l >> 5): the order in which a transposed 32x32 accumulator tile holds its 32 rows
   // (register r = (r & 3) + 8 (r >> 2) + 4 (l >> 5)), so such accumulators feed this
   // weight's MFMAs as the A operand without a shuffle (bottleneck_tail).
-  void* pack_frag_acc(const std::vector<float>& w, int N, int K) {
+  // kacc >= 0: only the k-steps below kacc in that order, the rest in pack_frag's (the in-tail
+  // shortcut's x fragments, BottleneckTailArgs::xsc)
+  void* pack_frag_acc(const std::vector<float>& w, int N, int K, int kacc = -1) {
     const int KS = K / 16, NT = N / 32;
     std::vector<uint16_t> pk((size_t)KS * 2 * NT * 64 * 8);
     for (int ks = 0; ks < KS; ++ks)
       for (int jt = 0; jt < NT; ++jt)
         for (int l = 0; l < 64; ++l)
           for (int e = 0; e < 8; ++e) {
-            const int k = ks * 16 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+            const int k = kacc >= 0 && ks * 16 >= kacc ? ks * 16 + 8 * (l >> 5) + e
+                                                        : ks * 16 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
             const float v = w[(size_t)(jt * 32 + (l & 31)) * K + k];
             const uint16_t hi = f2bf(v), lo = f2bf(v - bf2f(hi));
             const size_t o = (((size_t)ks * 2 * NT + jt) * 64 + l) * 8 + e;
@@ -568,6 +577,24 @@ struct Model::Impl {
           }
           rb.c3sc = pack_conv(wf, N, K, 1, bf.data(), "");
         }
+        if (bottleneck && rb.has_sc && rb.stride == 1 && rb.in_planes == rb.planes && rb.planes == 32 && rb.w3acc) {
+          std::vector<double> s3, h3, ss, hs;
+          bn_affine(p + ".bn3", s3, h3);
+          bn_affine(p + ".shortcut.1", ss, hs);
+          const std::vector<float>& w3 = P(p + ".conv3.weight");
+          const std::vector<float>& wsc = P(p + ".shortcut.0.weight");
+          const int C = rb.planes, K = 2 * C, N = rb.out_planes;
+          std::vector<float> wf((size_t)N * K), bf(N);
+          for (int n = 0; n < N; ++n) {
+            for (int k = 0; k < C; ++k) {
+              wf[(size_t)n * K + k] = (float)(w3[(size_t)n * C + k] * s3[n]);
+              wf[(size_t)n * K + C + k] = (float)(wsc[(size_t)n * C + k] * ss[n]);
+            }
+            bf[n] = (float)h3[n] + (float)hs[n];
+          }
+          rb.w3scx = pack_frag_acc(wf, N, K, C);
+          rb.b3scx = dev.upload(bf);
+        }
       }
     // seg_1 over TSTP stats; reference flatten index s*C*F4 + c*F4 + f, ours f*2C + s*C + c
     const int C4 = rblocks.back().out_planes, F4 = feat_dim / 8;
@@ -746,9 +773,19 @@ struct Model::Impl {
         const int Fo = (Fi - 1) / rb.stride + 1, To = (Ti - 1) / rb.stride + 1;
         const float* res = x;
         const bool tail = bottleneck && rb.stride == 1 && res_tail && rb.w3acc && img_ok(rb.c2, rb.planes);
+        const RBlock* nx = (size_t)ib < rblocks.size() ? &rblocks[ib] : nullptr;
+        // the tail also runs the next block's conv1 on this block's output (res_tail 1; the next
+        // block's conv2 reads y1 from either buffer); at a stage transition the next (first)
+        // block's conv1 is 4C -> 2C at this stage's resolution (option c1_stage_fuse)
+        const bool fuse1 =
+            tail && res_tail == 1 && nx && nx->w1frag &&
+            ((nx->planes == rb.planes && nx->w3acc && nx->stride == 1 && img_ok(nx->c2, nx->planes)) ||
+             (c1_stage_fuse && nx->planes == 2 * rb.planes && nx->in_planes == rb.out_planes && rb.planes <= 64));
         // conv3 + shortcut in one GEMM on the non-tail path (sc_fuse): no SC round trip through HBM
-        const bool fuse_sc = bottleneck && rb.has_sc && !tail && sc_fuse && rb.c3sc.w && x3_variant == 7;
-        if (rb.has_sc && !fuse_sc) {
+        const bool fuse_sc = bottleneck && rb.has_sc && !tail && (sc_fuse & 1) && rb.c3sc.w && x3_variant == 7;
+        // ... and inside the tail's conv3 for a stride-1 first block of 32 planes (w3scx)
+        const bool tail_sc = fuse1 && (sc_fuse & 2) && rb.w3scx && nx->planes == rb.planes;
+        if (rb.has_sc && !fuse_sc && !tail_sc) {
           gemm2d("shortcut", rb.sc, x, Ci, SC, rb.out_planes, nb, Fi, Ti, 1, rb.stride, 0, kActNone, nullptr, 0, s);
           res = SC;
         }
@@ -758,15 +795,8 @@ struct Model::Impl {
           y1_ready = false;
           if (tail) {
             // conv2 + conv3 + residual in one launch, y2 in registers (bottleneck_tail); with
-            // res_tail 1 also the next block's conv1 on this block's output (into the buffer
-            // the tail does not read)
-            const RBlock* nx = (size_t)ib < rblocks.size() ? &rblocks[ib] : nullptr;
-            // (the next block's conv2 reads y1 from either buffer); at a stage transition the next
-            // (first) block's conv1 is 4C -> 2C at this stage's resolution (option c1_stage_fuse)
-            const bool fuse1 =
-                res_tail == 1 && nx && nx->w1frag &&
-                ((nx->planes == rb.planes && nx->w3acc && nx->stride == 1 && img_ok(nx->c2, nx->planes)) ||
-                 (c1_stage_fuse && nx->planes == 2 * rb.planes && nx->in_planes == rb.out_planes && rb.planes <= 64));
+            // fuse1 also the next block's conv1 on this block's output (into the buffer the tail
+            // does not read)
             BottleneckTailArgs a{y1, res, o, nb, Fi, Ti, rb.c2.frag, rb.c2.bias, rb.w3acc, rb.c3.bias};
             float* y1n = y1 == Y1 ? Y2 : Y1;
             if (fuse1) {
@@ -775,9 +805,18 @@ struct Model::Impl {
               a.y1n = y1n;
               a.c1n = nx->planes;
             }
+            if (tail_sc) {
+              a.res = nullptr;
+              a.xsc = x;
+              a.w3 = rb.w3scx;
+              a.b3 = rb.b3scx;
+            }
             const double pos = (double)nb * Fi * Ti;
-            run(kTl[li], 2.0 * pos * (rb.c2.N * rb.c2.K + rb.c3.N * rb.c3.K + (fuse1 ? nx->c1.N * nx->c1.K : 0)), s,
-                [&] { launch_bottleneck_tail(a, rb.planes, s); });
+            run(kTl[li],
+                2.0 * pos *
+                    (rb.c2.N * rb.c2.K + rb.c3.N * rb.c3.K + (fuse1 ? nx->c1.N * nx->c1.K : 0) +
+                     (tail_sc ? rb.sc.N * rb.sc.K : 0)),
+                s, [&] { launch_bottleneck_tail(a, rb.planes, s); });
             if (fuse1) {
               y1_ready = true;
               y1_next = y1n;
